@@ -1,0 +1,201 @@
+"""bench.py — propagation steps/s of the 4-level biexciton PT propagator at bond dimension 64.
+
+Workload (BASELINE.json metric): every rank runs the two-time G2(t1, tau)
+sweep of the biexciton cascade (N=4, delta_b=4, lindblad, dt=0.1 ps, pulse train
+PulseTrain(100, 10, ChirpedPulse(tau_0=3, e_start=-2, e0, t0=12))), with a chi=64 synthetic PT
+(I + 0.05 G/sqrt(chi) per slice, spectral radius <= 1, 410 initial slices + 1 repeated
+slice, no dictionary compression: D = N^2 = 16). n_traj t1 points (t1 = 0, 0.1, ... ps), each a
+trajectory with the MTOs A=|3><1| (right) and C=|1><3| (left) at t1 and outputs <B>=<|1><1|> and
+<ABC> over tau = 0..1000 ps (n_tau = 10,000). Ranks form a pulse-area scan (e0 = 1 + 0.1 rank), so the
+per-GPU work is fixed (weak scaling) and there is no data-path collective.
+
+One bench step = one execution of the device-resident plan: free-propagator build for all 2*n_steps
+half steps + the lock-step PT sweep of all trajectories. Inputs (PT, operators, pulse samples) are
+resident in HBM before the timed region. value = whole-job useful trajectory-steps per second
+(n_traj * n_tau per rank; the redundant trunk re-propagation 0 -> t1 is executed but not counted).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 (vector == matrix on gfx950), spec
+PEAK_HBM_GBS = 8000.0
+
+
+def build_workload(n_traj, n_tau, chi, rank=0, dt=0.1, seed=1234):
+    from pyaceqd_amd import engine, opgrammar, pt as ptmod
+    from pyaceqd_amd.constants import hbar
+    from pyaceqd_amd.four_level_system.linear import biexciton_ops
+    from pyaceqd_amd.pulses import ChirpedPulse, PulseTrain
+    N = 4
+    so, bo, lo, io, _ = biexciton_ops(delta_b=4, lindblad=True)
+    t1_steps = np.arange(n_traj)
+    n_steps = int(t1_steps[-1] + n_tau)
+    ds = dt / 4
+    ts = ds * np.arange(4 * n_steps + 1)
+    e0 = 1.0 + 0.1 * rank
+    train = PulseTrain(100, 10, ChirpedPulse(tau_0=3, e_start=-2.0, e0=e0, t0=12, polar_x=1.0))
+    fx, fy = train.get_total_xy(ts)
+    mat = lambda s: opgrammar.to_matrix(s, N)  # noqa: E731
+    chans = [(-0.5 * np.pi * hbar * mat(op), fx if pol == "x" else fy) for op, pol in io]
+    sysd = engine.System(dim=N, H0=sum(mat(s) for s in so), lindblad=[(r, mat(o)) for o, r in lo],
+                         channels=chans, sample_t0=0.0, sample_dt=ds)
+    grid = engine.Grid(0.0, dt, n_steps, 1)
+    pt = ptmod.synthetic_pt(mat(bo), chi=chi, n_init=min(410, n_steps), n_rep=1, seed=seed, eps=0.05, dt=dt)
+    A, B, Cm = mat("|3><1|_4"), mat("|1><1|_4"), mat("|1><3|_4")
+    mtos = []
+    for t in range(n_traj):
+        mtos.append(engine.MTO(t, int(t1_steps[t]), False, 2, A))
+        mtos.append(engine.MTO(t, int(t1_steps[t]), False, 1, Cm))
+    tr = engine.Trajectories(t1_steps.copy(), t1_steps + n_tau, mtos)
+    ops = [B, A @ B @ Cm]
+    rho0 = mat("|0><0|_4")
+    return sysd, grid, pt, rho0, ops, tr
+
+
+def flops_per_traj_step(N=4, chi=64, n_out=2):
+    """F = 8 (D chi^2 + 2 chi N^4 + n_out N^2), D = N^2 PT rows contracted per step"""
+    D = N * N
+    return 8 * (D * chi * chi + 2 * chi * N ** 4 + n_out * N * N)
+
+
+def bytes_per_launch(n_steps, n_init, chi, N=4, n_out=2, n_traj=1, D=16, executed_steps=0):
+    """unique HBM bytes one sweep launch must move: every distinct PT slice once, both free propagators
+    per step, per-trajectory outputs written, augmented states never leave LDS"""
+    slices = min(n_steps, n_init) + 1
+    return slices * D * chi * chi * 16 + 2 * n_steps * (N * N) ** 2 * 16 + n_out * 16 * executed_steps
+
+
+def cpu_baseline(chi, target_s=15.0):
+    """oracle/liboracle.so (plain-C port, OpenMP over trajectories) on a bounded sample of the same workload"""
+    from oracle import oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    threads = max(1, min(threads, 16))
+    # calibrate on 1 trajectory x 60 steps
+    sysd, grid, pt, rho0, ops, tr = build_workload(1, 60, chi)
+    t0 = time.perf_counter()
+    oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt, nthreads=1)
+    per = (time.perf_counter() - t0) / 61
+    n_traj = 2 * threads
+    steps = int(max(50, min(10000, target_s * threads / per / n_traj)))
+    sysd, grid, pt, rho0, ops, tr = build_workload(n_traj, steps, chi)
+    t0 = time.perf_counter()
+    oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt, nthreads=threads)
+    el = time.perf_counter() - t0
+    executed = int(np.sum(tr.out_end + 1))
+    return {"value": executed / el, "unit": "traj-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{n_traj} trajectories x {steps} tau-steps (executed {executed} traj-steps incl. trunk and "
+                      f"free-propagator build), chi={chi}, N=4, {el:.1f} s, oracle/pqd_oracle.c OpenMP"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--traj", type=int, default=1024, help="t1 trajectories per GPU")
+    ap.add_argument("--n-tau", type=int, default=10000)
+    ap.add_argument("--chi", type=int, default=64)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+    import torch
+
+    from pyaceqd_amd import _lib, engine
+    ctx = _lib.context(local)
+    sysd, grid, pt, rho0, ops, tr = build_workload(args.traj, args.n_tau, args.chi, rank=rank)
+    plan = engine.Plan(sysd, grid, rho0, ops, tr, pt=pt, ctx=ctx)
+
+    def barrier():
+        if dist is not None:
+            if torch.cuda.is_available():
+                dist.barrier(device_ids=[local])
+            else:
+                dist.barrier()
+
+    for _ in range(args.warmup):
+        plan.execute()
+    plan.synchronize()
+    plan.timing(reset=True)
+    barrier()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        plan.execute()
+    plan.synchronize()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    ms_free, ms_sweep, nexec = plan.timing(reset=True)
+    if dist is not None:
+        t = torch.tensor([el, ms_sweep, ms_free], dtype=torch.float64,
+                         device=f"cuda:{local}" if torch.cuda.is_available() else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el, ms_sweep, ms_free = [float(x) for x in t.tolist()]
+
+    # sanity on the last result (outside the timed region): trace-free check of <B> bounds
+    res = plan.download()
+    g0 = np.array([r[0, 1] for r in res])
+    assert np.all(np.isfinite(g0)), "non-finite output"
+
+    useful = args.traj * args.n_tau
+    executed = int(np.sum(tr.out_end + 1))
+    value = useful * args.steps * world / el
+    F = flops_per_traj_step(4, args.chi, len(ops))
+    achieved_tf = executed * F / (ms_sweep * 1e-3) / 1e12
+    line = {
+        "metric": "propagation steps/sec (whole node), 4-level biexciton PT bond-dim 64",
+        "value": value,
+        "unit": "traj-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "c128 (fp64)",
+        "data": "synthetic (SURVEY.md §8d: pulse train + synthetic chi=64 PT)",
+        "config": {"workload": "biexciton two-time G2 sweep (C3 metric config, C4 shape, C5 scan over ranks)",
+                   "N": 4, "chi": args.chi, "D": 16, "dt_ps": 0.1, "n_tau": args.n_tau,
+                   "traj_per_gpu": args.traj, "grid_steps": grid.n_steps,
+                   "useful_traj_steps_per_gpu": useful, "executed_traj_steps_per_gpu": executed,
+                   "parallelism": f"scan{world}", "kernel_ms": {"pt_sweep": ms_sweep, "free_prop": ms_free}},
+        "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved_tf / PEAK_FP64_TFLOPS, "traffic": None,
+                     "kernel": "pt_sweep_kernel<16,64>",
+                     "algorithmic": f"{F} flop/traj-step x {executed} executed traj-steps per launch",
+                     "hbm_algorithmic_GBs": bytes_per_launch(grid.n_steps, 410, args.chi, n_traj=args.traj,
+                                                             executed_steps=executed) / (ms_sweep * 1e-3) / 1e9},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.chi, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

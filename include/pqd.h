@@ -1,0 +1,168 @@
+/* pqd.h — C-ABI of libpqd, the MI355X-native process-tensor propagator behind pyaceqd's
+ * `system_ace_stream` driver and its two-time sweeps.
+ *
+ * Drop-in boundary. Each entry point replaces one reference interface:
+ *
+ *   pqd_propagate / pqd_plan_*      replace the ACE engine process boundary
+ *                                   `subprocess.check_output(["ACE", param_file])` + outfile parse
+ *                                   (pyaceqd/general_system/general_system.py:337-343, params :227-290,
+ *                                   parse read_result :104-110), batched over trajectories so the
+ *                                   ThreadPoolExecutor fan-out of two_time/correlations.py:153-169 becomes
+ *                                   one launch.
+ *   pqd_pt_create                   replaces `add_PT <file>` + the PT files ACE writes
+ *                                   (general_system.py:146-197, 236); device-resident, shared per context.
+ *   pqd_free_propagators            exposes the free propagator ACEutils.FreePropagator.update(t,dt).M
+ *                                   (general_system.py:324-327, `get_M_t`).
+ *   pqd_propagate_tau               f2py propagate_tau_module.propagate_tau   (two_time/propagate_tau.f90:3)
+ *   pqd_calc_onetime_parallel       ... .calc_onetime_parallel                 (propagate_tau.f90:110)
+ *   pqd_calc_onetime_parallel_block ... .calc_onetime_parallel_block           (propagate_tau.f90:189)
+ *   pqd_calc_twotime_phonon_block   ... .calc_twotime_phonon_block             (propagate_tau.f90:374)
+ *   pqd_four_time_8op               f2py timebin_tl.four_time_8op              (timebin/timebin_tl.f90:216)
+ *   pqd_four_time                   ... .four_time                             (timebin_tl.f90:145)
+ *   pqd_dynamics_t1                 ... .dynamics_t1                           (timebin_tl.f90:305)
+ *
+ * Conventions: complex numbers are interleaved doubles {re, im}; N x N operators row-major;
+ * Liouville vectors row-major vec(rho)[i*N+j] = rho[i][j]; map-chain arguments keep the
+ * reference's Fortran (column-major) layouts and index semantics, with the f2py-hidden
+ * dimensions passed explicitly. All host buffers are caller-owned. Every function returns 0 on
+ * success or a PQD_ERR_* code; pqd_last_error() (thread-local) describes the last failure.
+ * Nothing here ever calls exit().
+ */
+#ifndef PQD_H
+#define PQD_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PQD_OK 0
+#define PQD_ERR_ARG 1
+#define PQD_ERR_HIP 2
+#define PQD_ERR_UNSUPPORTED 3
+#define PQD_ERR_NOMEM 4
+#define PQD_ERR_NUMERIC 5
+
+typedef struct { double re, im; } pqd_c128;
+typedef struct pqd_ctx pqd_ctx;
+typedef struct pqd_pt pqd_pt;
+typedef struct pqd_plan pqd_plan;
+
+/* The system: what the param file's add_Hamiltonian / add_Lindblad / add_Pulse lines say
+ * (general_system.py:241-279). H(t) = H0 + sum_p (f_p(t) X_p + conj(f_p(t)) X_p^dagger). */
+typedef struct {
+    int32_t dim;                 /* N (Hilbert-space dimension) */
+    double hbar;                 /* meV ps, constants.py:1 */
+    const pqd_c128* H0;          /* N*N */
+    int32_t n_lind;
+    const double* lind_rates;    /* n_lind       (add_Lindblad <rate> {L}) */
+    const pqd_c128* lind_ops;    /* n_lind*N*N */
+    int32_t n_chan;              /* pulse / rotating-frame channels */
+    const pqd_c128* chan_ops;    /* n_chan*N*N: X_p (already scaled, e.g. -0.5*pi*hbar*op) */
+    const pqd_c128* chan_samples;/* n_chan*n_samples: f_p at sample_t0 + k*sample_dt */
+    int32_t n_samples;
+    double sample_t0, sample_dt; /* linear interpolation, clamped at both ends */
+} pqd_system;
+
+/* dt / ta / te of the param file; n_steps = round((te-ta)/dt). Output rows are steps 0..n_steps. */
+typedef struct {
+    double ta, dt;
+    int32_t n_steps;
+    int32_t n_sub;               /* exponential-midpoint sub-steps per half step (>= 1) */
+} pqd_grid;
+
+/* Process-tensor MPO for a diagonal system-bath coupling: per slice s and dictionary index g a
+ * chi x chi matrix Q[s][g][d][d']; g = gmap[alpha] for Liouville index alpha. */
+typedef struct {
+    int32_t chi, D, n_slices;
+    const pqd_c128* Q;           /* n_slices*D*chi*chi */
+    const pqd_c128* closure;     /* n_slices*chi: bond closure after a step that used slice s */
+    const pqd_c128* closure0;    /* chi: closure for the output at step 0 */
+    const pqd_c128* bond0;       /* chi: initial bond vector */
+    const int32_t* gmap;         /* N*N */
+} pqd_pt_desc;
+
+/* A batch of trajectories sharing system, grid, PT and initial state. Trajectory t is propagated
+ * from step 0 to out_end[t] and writes n_out expectation values per step of [out_begin, out_end]
+ * to out[out_offset[t] + (n - out_begin[t])*n_out + k]. MTOs = apply_Operator lines
+ * (general_system.py:281-286): kind 0 "" (A rho A^dag), 1 "_left" (A rho), 2 "_right" (rho A);
+ * before=1 is applyBefore true (visible at step), 0 visible one step later; same (traj, step,
+ * before) operators apply in array order. */
+typedef struct {
+    int32_t n_traj;
+    const int32_t* out_begin;
+    const int32_t* out_end;
+    const int64_t* out_offset;
+    int32_t n_mto;
+    const int32_t* mto_traj;
+    const int32_t* mto_step;
+    const int32_t* mto_before;
+    const int32_t* mto_kind;
+    const pqd_c128* mto_ops;     /* n_mto*N*N */
+} pqd_traj;
+
+int32_t pqd_version(void);
+const char* pqd_last_error(void);
+
+int pqd_ctx_create(int32_t device, pqd_ctx** out);
+void pqd_ctx_destroy(pqd_ctx* ctx);
+int pqd_ctx_synchronize(pqd_ctx* ctx);
+
+int pqd_pt_create(pqd_ctx* ctx, int32_t dim, const pqd_pt_desc* desc, pqd_pt** out);
+void pqd_pt_destroy(pqd_pt* pt);
+
+/* M_out: 2*n_steps matrices (N^2 x N^2, row-major): [2n] first half step, [2n+1] second. */
+int pqd_free_propagators(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* grid, pqd_c128* M_out);
+
+/* one-shot: upload, propagate, download. pt may be NULL (no phonons); sched[n_steps] selects the
+ * PT slice per step (NULL: min(n, n_slices-1)). rho0: N*N. out_ops: n_out*N*N. */
+int pqd_propagate(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* grid, const pqd_pt* pt,
+                  const int32_t* sched, const pqd_c128* rho0, int32_t n_out, const pqd_c128* out_ops,
+                  const pqd_traj* traj, pqd_c128* out, int64_t out_len);
+
+/* device-resident plan for repeated execution (bench, scans): same arguments as pqd_propagate. */
+int pqd_plan_create(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* grid, const pqd_pt* pt,
+                    const int32_t* sched, const pqd_c128* rho0, int32_t n_out, const pqd_c128* out_ops,
+                    const pqd_traj* traj, int64_t out_len, pqd_plan** out);
+/* enqueue free-propagator build (if rebuild_free) + sweep on the context stream (asynchronous) */
+int pqd_plan_execute(pqd_plan* plan, int32_t rebuild_free);
+/* device pointer of the plan's output buffer (out_len complex values) */
+void* pqd_plan_output_device(pqd_plan* plan);
+int pqd_plan_download(pqd_plan* plan, pqd_c128* out, int64_t out_len);
+/* average kernel durations (ms) of the executions since the last reset, from HIP events on the
+ * launch stream: [0] free-propagator kernel, [1] sweep kernel; n = number of executions */
+int pqd_plan_timing(pqd_plan* plan, double* ms_free, double* ms_sweep, int32_t* n, int32_t reset);
+void pqd_plan_destroy(pqd_plan* plan);
+
+/* ---- map-chain sweeps: reference Fortran signatures, hidden dims explicit, Fortran layouts ---- */
+int pqd_propagate_tau(pqd_ctx* ctx, const pqd_c128* dm_tl, int32_t n_maps, const pqd_c128* rho_init,
+                      int32_t n_tau, int32_t dim, int32_t j_start, pqd_c128* rho_out);
+int pqd_calc_onetime_parallel(pqd_ctx* ctx, const pqd_c128* dm_tl, const pqd_c128* rho_init, int32_t n_tau,
+                              int32_t n_t, int32_t n_tfull, int32_t dim, const pqd_c128* opA,
+                              const pqd_c128* opB, const pqd_c128* opC, const double* time,
+                              const double* time_sparse, pqd_c128* result);
+int pqd_calc_onetime_parallel_block(pqd_ctx* ctx, const pqd_c128* dm_block, const pqd_c128* dm_s,
+                                    const pqd_c128* rho_init, int32_t n_tb, int32_t nx_tau, int32_t n_map,
+                                    int32_t n_t, int32_t n_tfull, int32_t dim, const pqd_c128* opA,
+                                    const pqd_c128* opB, const pqd_c128* opC, const double* time,
+                                    const double* time_sparse, pqd_c128* result);
+int pqd_calc_twotime_phonon_block(pqd_ctx* ctx, const pqd_c128* dm_taucs2, const pqd_c128* dm_sep1,
+                                  const pqd_c128* dm_sep2, const pqd_c128* dm_s, const pqd_c128* rho_init,
+                                  int32_t n_tb, int32_t nx_tau, int32_t n_map, int32_t n_t, int32_t n_tfull,
+                                  int32_t n_tauc, int32_t dim, const pqd_c128* opA, const pqd_c128* opB,
+                                  const pqd_c128* opC, const double* time, const double* time_sparse,
+                                  pqd_c128* result);
+int pqd_four_time_8op(pqd_ctx* ctx, const pqd_c128* dm_1, const pqd_c128* dm_2, const pqd_c128* rho_init,
+                      const double* t1, const pqd_c128* precalc, int32_t n_t, double dt, int32_t n_map,
+                      int32_t dim, const pqd_c128* ops8, int32_t early_only, int32_t late_t1_only, double tb,
+                      int32_t n_precalc, pqd_c128* result);
+int pqd_four_time(pqd_ctx* ctx, const pqd_c128* dm_1, const pqd_c128* dm_2, const pqd_c128* rho_init,
+                  const double* t1, const pqd_c128* precalc, int32_t n_t, double dt, int32_t n_map, int32_t dim,
+                  const pqd_c128* ops4, double tb, int32_t n_precalc, pqd_c128* result);
+int pqd_dynamics_t1(pqd_ctx* ctx, const pqd_c128* dm_1, const pqd_c128* dm_2, const pqd_c128* rho_init,
+                    const double* t1, const pqd_c128* precalc, int32_t n_t, double dt, int32_t n_map,
+                    int32_t dim, double tb, int32_t n_precalc, pqd_c128* result);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,154 @@
+// free_prop.hip — batched free propagators M(n,h) = prod_j exp(L(t_j) w), one workgroup per matrix.
+//
+// Replaces the free-propagator construction ACE performs for every step from the param lines
+// add_Hamiltonian / add_Pulse (+h.c.) / add_Lindblad (general_system.py:241-279, symmetric Trotter
+// :234) and that ACEutils exposes as FreePropagator.update(t, dt).M (general_system.py:324-327).
+// All trajectories at the same absolute step share these matrices, so they are built once per
+// step here (2 * n_steps independent N2 x N2 expm's: 16x16 at N=4, 36x36 at N=6).
+//
+// Algorithm per matrix (same as the oracle's or_expm): A = L(t) w, s = max(0, e) with
+// frexp(||A||_1 / 0.5) = m 2^e, degree-18 Taylor polynomial by Horner on A 2^-s, then s squarings.
+// The N2 x N2 operands live in LDS; each of the 256 threads owns ceil(N2^2/256) output entries.
+#include "pqd_common.h"
+
+namespace {
+
+__device__ __forceinline__ double2 sample_ch(const FreePropParams& p, int c, double t) {
+    const double2* f = p.samples + (size_t)c * p.n_samples;
+    const int ns = p.n_samples;
+    const double u = (t - p.s_t0) / p.s_dt;
+    if (!(u > 0.0)) return f[0];
+    if (u >= (double)(ns - 1)) return f[ns - 1];
+    const int k = (int)floor(u);
+    const double w = u - (double)k;
+    const double2 a = f[k], b = f[k + 1];
+    return make_double2(a.x + w * (b.x - a.x), a.y + w * (b.y - a.y));
+}
+
+template <int N2>
+__device__ __forceinline__ void lds_matmul(const double2* A, const double2* B, double2* C, int tid) {
+    for (int e = tid; e < N2 * N2; e += 256) {
+        const int i = e / N2, j = e - i * N2;
+        double2 acc = c_zero();
+#pragma unroll 4
+        for (int k = 0; k < N2; ++k) c_fma(acc, A[i * N2 + k], B[k * N2 + j]);
+        C[e] = acc;
+    }
+}
+
+template <int N2>
+__global__ __launch_bounds__(256) void free_prop_kernel(FreePropParams p) {
+    extern __shared__ __attribute__((aligned(16))) double2 smem[];
+    double2* A = smem;
+    double2* P = A + N2 * N2;
+    double2* T = P + N2 * N2;
+    double2* Acc = T + N2 * N2;
+    __shared__ double colsum[N2];
+    __shared__ int s_sh;
+
+    const int tid = threadIdx.x;
+    const int m = blockIdx.x;
+    const int n = m >> 1, h = m & 1;
+    const int nsub = p.n_sub > 0 ? p.n_sub : 1;
+    const double w = 0.5 * p.dt / nsub;
+
+    for (int j = 0; j < nsub; ++j) {
+        const double t = p.ta + n * p.dt + h * 0.5 * p.dt + (j + 0.5) * w;
+        double2 f[4], fc[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (c < p.n_chan) { f[c] = sample_ch(p, c, t); fc[c] = c_conj(f[c]); }
+        }
+        for (int e = tid; e < N2 * N2; e += 256) {
+            double2 v = p.L0[e];
+            for (int c = 0; c < p.n_chan; ++c) {
+                c_fma(v, f[c], p.S[(size_t)c * N2 * N2 + e]);
+                c_fma(v, fc[c], p.T[(size_t)c * N2 * N2 + e]);
+            }
+            A[e] = c_scale(v, w);
+        }
+        __syncthreads();
+        if (tid < N2) {
+            double s = 0.0;
+            for (int r = 0; r < N2; ++r) { const double2 a = A[r * N2 + tid]; s += hypot(a.x, a.y); }
+            colsum[tid] = s;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            double norm = 0.0;
+            for (int c = 0; c < N2; ++c) norm = colsum[c] > norm ? colsum[c] : norm;
+            int e2 = 0;
+            frexp(norm / 0.5, &e2);
+            s_sh = e2 > 0 ? e2 : 0;
+        }
+        __syncthreads();
+        const int s = s_sh;
+        const double scale = ldexp(1.0, -s);
+        for (int e = tid; e < N2 * N2; e += 256) {
+            const double2 a = c_scale(A[e], scale);
+            A[e] = a;
+            double2 pv = make_double2(a.x / 18.0, a.y / 18.0);
+            const int i = e / N2;
+            if (e == i * N2 + i) pv.x += 1.0;
+            P[e] = pv;
+        }
+        __syncthreads();
+        for (int mm = 17; mm >= 1; --mm) {
+            lds_matmul<N2>(A, P, T, tid);
+            __syncthreads();
+            for (int e = tid; e < N2 * N2; e += 256) {
+                const double2 tv = T[e];
+                double2 pv = make_double2(tv.x / (double)mm, tv.y / (double)mm);
+                const int i = e / N2;
+                if (e == i * N2 + i) pv.x += 1.0;
+                P[e] = pv;
+            }
+            __syncthreads();
+        }
+        for (int q = 0; q < s; ++q) {
+            lds_matmul<N2>(P, P, T, tid);
+            __syncthreads();
+            for (int e = tid; e < N2 * N2; e += 256) P[e] = T[e];
+            __syncthreads();
+        }
+        if (j == 0) {
+            for (int e = tid; e < N2 * N2; e += 256) Acc[e] = P[e];
+        } else {
+            lds_matmul<N2>(P, Acc, T, tid);
+            __syncthreads();
+            for (int e = tid; e < N2 * N2; e += 256) Acc[e] = T[e];
+        }
+        __syncthreads();
+    }
+    double2* out = p.M + (size_t)m * N2 * N2;
+    for (int e = tid; e < N2 * N2; e += 256) out[e] = Acc[e];
+}
+
+template <int N2>
+hipError_t launch_fp(const FreePropParams& p, hipStream_t s) {
+    const size_t lds = 4ull * N2 * N2 * sizeof(double2);
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)free_prop_kernel<N2>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    const int nblk = 2 * p.n_steps;
+    if (nblk <= 0) return hipSuccess;
+    hipLaunchKernelGGL(free_prop_kernel<N2>, dim3(nblk), dim3(256), lds, s, p);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_free_prop(int N2, const FreePropParams& p, hipStream_t s) {
+    switch (N2) {
+        case 4: return launch_fp<4>(p, s);
+        case 9: return launch_fp<9>(p, s);
+        case 16: return launch_fp<16>(p, s);
+        case 25: return launch_fp<25>(p, s);
+        case 36: return launch_fp<36>(p, s);
+        default: return hipErrorInvalidValue;
+    }
+}

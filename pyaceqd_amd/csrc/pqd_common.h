@@ -1,0 +1,109 @@
+// pqd_common.h — shared device/host definitions for libpqd (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PQD_WAVE 64
+
+// ---------------------------------------------------------------------------------------------
+// complex double helpers (interleaved re, im == pqd_c128 == double2)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ double2 c_zero() { return make_double2(0.0, 0.0); }
+__device__ __forceinline__ double2 c_add(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 c_sub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double2 c_scale(double2 a, double s) { return make_double2(a.x * s, a.y * s); }
+__device__ __forceinline__ double2 c_conj(double2 a) { return make_double2(a.x, -a.y); }
+__device__ __forceinline__ double2 c_mul(double2 a, double2 b) {
+    return make_double2(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
+}
+// acc += a * b  (4 FMAs)
+__device__ __forceinline__ void c_fma(double2& acc, double2 a, double2 b) {
+    acc.x = fma(a.x, b.x, acc.x);
+    acc.x = fma(-a.y, b.y, acc.x);
+    acc.y = fma(a.x, b.y, acc.y);
+    acc.y = fma(a.y, b.x, acc.y);
+}
+__device__ __forceinline__ double2 c_shfl_xor(double2 v, int m) {
+    return make_double2(__shfl_xor(v.x, m), __shfl_xor(v.y, m));
+}
+
+// ---------------------------------------------------------------------------------------------
+// kernel parameter blocks (passed by value)
+// ---------------------------------------------------------------------------------------------
+struct FreePropParams {
+    const double2* L0;       // N2*N2 constant Liouvillian (H0 commutator + dissipators), row-major
+    const double2* S;        // n_chan*N2*N2 superoperator of -i/hbar [X_p, .]
+    const double2* T;        // n_chan*N2*N2 superoperator of -i/hbar [X_p^dagger, .]
+    const double2* samples;  // n_chan*n_samples
+    int n_chan, n_samples;
+    double s_t0, s_dt;
+    double ta, dt;
+    int n_steps, n_sub;
+    double2* M;              // out: 2*n_steps*N2*N2
+};
+
+struct SweepParams {
+    const double2* M;        // 2*n_steps*N2*N2 free propagators
+    const double2* Q;        // PT slices n_slices*D*CHI*CHI (chi padded to CHI)
+    int D;
+    const int* sched;        // n_steps
+    const double2* closure;  // n_slices*CHI
+    const double2* closure0; // CHI
+    const double2* bond0;    // CHI
+    const int* gmap;         // N2
+    const double2* rho0;     // N2 (row-major vec)
+    int n_out;
+    const double2* ovec;     // n_out*N2: ovec[k][i*N+j] = O_k[j][i]  => <O_k> = sum_a ovec[k][a] r[a]
+    const int* blk_traj;     // n_blocks*4 trajectory ids (-1: empty slot)
+    const int* blk_end;      // n_blocks: last step of the block (max out_end)
+    const int* wbeg;         // per trajectory
+    const int* wend;
+    const long long* woff;
+    const int* ev_start;     // n_traj+1
+    const int4* ev;          // (step, after?1:0, superop index, 0), sorted per trajectory
+    const double2* sop;      // MTO superoperators N2*N2 each
+    double2* out;
+};
+
+// map-chain (Fortran f2py equivalents)
+struct MapChainParams {
+    int mode;                // 0 onetime, 1 onetime_block, 2 twotime_phonon_block
+    int dim, N2;
+    const double2* dmA;      // mode0: dm_tl   mode1: dm_block   mode2: dm_sep1
+    const double2* dmB;      // mode2: dm_sep2
+    const double2* dmT;      // mode2: dm_taucs2 (N2,N2,n_tauc,n_map)
+    const double2* dm_s;     // mode1/2 stationary map
+    int n_map, n_tb, nx_tau, n_tauc;
+    const double2* rho_init;
+    const double2* opA; const double2* opB; const double2* opC;   // Fortran column-major dim x dim
+    const double* time; const double* time_sparse;
+    int n_t, n_tfull, n_tau;  // n_tau: number of tau columns after the first (ncol-1)
+    double2* rho_buf;        // scratch n_t*N2
+    int* j_arr;              // scratch n_t
+    double2* result;         // (n_t, n_tau+1) column-major
+};
+
+struct FourTimeParams {
+    int dim, N2, n_t, n_map, n_precalc;
+    double dt, tb;
+    const double2* dm1; const double2* dm2; const double2* precalc;  // Fortran layouts
+    const double2* rho_init;
+    const double* t1;
+    const double2* ops;      // 8 (or 4) Fortran dim x dim
+    int variant;             // 0: four_time_8op, 1: four_time (4 ops)
+    int early_only, late_t1_only;
+    const int2* pairs;       // (i, j) list
+    int n_pairs;
+    double2* result;         // (n_t, n_t) column-major
+};
+
+// launchers (defined in the .hip translation units)
+hipError_t launch_free_prop(int N2, const FreePropParams& p, hipStream_t s);
+hipError_t launch_sweep(int N2, int CHI, int n_blocks, const SweepParams& p, hipStream_t s);
+hipError_t launch_sweep_nopt(int N2, int n_blocks, const SweepParams& p, hipStream_t s);
+hipError_t launch_mapchain(const MapChainParams& p, hipStream_t s);
+hipError_t launch_four_time(const FourTimeParams& p, hipStream_t s);
+hipError_t launch_propagate_tau(int N2, const double2* dm, const double2* rho0, int n_tau, int j_start,
+                                double2* out, hipStream_t s);
+hipError_t launch_dynamics_t1(const FourTimeParams& p, double2* out, hipStream_t s);
+bool sweep_supported(int N2, int CHI);

@@ -1,0 +1,716 @@
+// pqd_host.cpp — C-ABI implementation of libpqd (include/pqd.h): validation, Liouvillian /
+// superoperator construction, MTO scheduling, trajectory grouping, device buffers, launches.
+// No arithmetic of the propagation itself happens on the host: the free propagators, the PT
+// sweep, traces and the map-chain sweeps all run in the HIP kernels (free_prop.hip, pt_sweep.hip,
+// mapchain.hip). Host code only assembles constant N^2 x N^2 generators from N x N operators.
+#include "../../include/pqd.h"
+#include "pqd_common.h"
+
+#include <algorithm>
+#include <memory>
+#include <complex>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+using cd = std::complex<double>;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(x)                                                                              \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) return fail(PQD_ERR_HIP, "%s: %s (%s:%d)", #x, hipGetErrorString(e_), \
+                                          __FILE__, __LINE__);                                 \
+    } while (0)
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    hipError_t alloc(size_t count) {
+        release();
+        n = count;
+        if (count == 0) return hipSuccess;
+        return hipMalloc((void**)&p, count * sizeof(T));
+    }
+    hipError_t upload(const T* src, size_t count, hipStream_t s) {
+        hipError_t e = alloc(count);
+        if (e != hipSuccess || count == 0) return e;
+        return hipMemcpyAsync(p, src, count * sizeof(T), hipMemcpyHostToDevice, s);
+    }
+};
+
+const cd* C(const pqd_c128* p) { return reinterpret_cast<const cd*>(p); }
+
+int pad_chi(int chi) {
+    if (chi <= 16) return 16;
+    if (chi <= 32) return 32;
+    if (chi <= 64) return 64;
+    return -1;
+}
+
+// ---- superoperators in the row-major vec convention: vec(A rho B) = (A (x) B^T) vec(rho)
+void kron_left(int N, const cd* A, cd* S, cd f) {  // S += f * (A (x) I)
+    const int N2 = N * N;
+    for (int i = 0; i < N; ++i)
+        for (int j = 0; j < N; ++j)
+            for (int k = 0; k < N; ++k) S[(size_t)(i * N + j) * N2 + (k * N + j)] += f * A[i * N + k];
+}
+void kron_right(int N, const cd* B, cd* S, cd f) {  // S += f * (I (x) B^T): rho -> rho B
+    const int N2 = N * N;
+    for (int i = 0; i < N; ++i)
+        for (int j = 0; j < N; ++j)
+            for (int l = 0; l < N; ++l) S[(size_t)(i * N + j) * N2 + (i * N + l)] += f * B[l * N + j];
+}
+void commutator(int N, const cd* H, double hbar, cd* S) {  // S += -i/hbar [H, .]
+    const cd f(0.0, -1.0 / hbar);
+    kron_left(N, H, S, f);
+    kron_right(N, H, S, -f);
+}
+void dissipator(int N, const cd* Lk, double g, cd* S) {  // S += g (L . L^dag - 1/2 {L^dag L, .})
+    const int N2 = N * N;
+    std::vector<cd> LdL(N * N);
+    for (int i = 0; i < N; ++i)
+        for (int j = 0; j < N; ++j) {
+            cd s = 0;
+            for (int k = 0; k < N; ++k) s += std::conj(Lk[k * N + i]) * Lk[k * N + j];
+            LdL[i * N + j] = s;
+        }
+    for (int i = 0; i < N; ++i)
+        for (int j = 0; j < N; ++j)
+            for (int k = 0; k < N; ++k)
+                for (int l = 0; l < N; ++l)
+                    S[(size_t)(i * N + j) * N2 + (k * N + l)] += g * Lk[i * N + k] * std::conj(Lk[j * N + l]);
+    kron_left(N, LdL.data(), S, cd(-0.5 * g));
+    kron_right(N, LdL.data(), S, cd(-0.5 * g));
+}
+void mto_superop(int N, int kind, const cd* A, cd* S) {
+    const int N2 = N * N;
+    std::fill(S, S + (size_t)N2 * N2, cd(0));
+    if (kind == 1) {
+        kron_left(N, A, S, 1.0);
+    } else if (kind == 2) {
+        kron_right(N, A, S, 1.0);
+    } else {  // A rho A^dag: A (x) conj(A)
+        for (int i = 0; i < N; ++i)
+            for (int j = 0; j < N; ++j)
+                for (int k = 0; k < N; ++k)
+                    for (int l = 0; l < N; ++l)
+                        S[(size_t)(i * N + j) * N2 + (k * N + l)] = A[i * N + k] * std::conj(A[j * N + l]);
+    }
+}
+void matmul_sq(int n, const cd* A, const cd* B, cd* Cm) {
+    std::vector<cd> t((size_t)n * n, 0.0);
+    for (int i = 0; i < n; ++i)
+        for (int k = 0; k < n; ++k) {
+            const cd a = A[(size_t)i * n + k];
+            for (int j = 0; j < n; ++j) t[(size_t)i * n + j] += a * B[(size_t)k * n + j];
+        }
+    std::copy(t.begin(), t.end(), Cm);
+}
+
+int check_system(const pqd_system* sys) {
+    if (!sys) return fail(PQD_ERR_ARG, "system is NULL");
+    if (sys->dim < 2 || sys->dim > 6) return fail(PQD_ERR_UNSUPPORTED, "dim %d not in [2, 6]", sys->dim);
+    if (!sys->H0) return fail(PQD_ERR_ARG, "H0 is NULL");
+    if (!(sys->hbar > 0)) return fail(PQD_ERR_ARG, "hbar must be > 0");
+    if (sys->n_lind < 0 || (sys->n_lind > 0 && (!sys->lind_ops || !sys->lind_rates)))
+        return fail(PQD_ERR_ARG, "bad Lindblad arguments");
+    if (sys->n_chan < 0 || sys->n_chan > 4) return fail(PQD_ERR_UNSUPPORTED, "n_chan %d not in [0, 4]", sys->n_chan);
+    if (sys->n_chan > 0 && (!sys->chan_ops || !sys->chan_samples || sys->n_samples < 1 || !(sys->sample_dt > 0)))
+        return fail(PQD_ERR_ARG, "bad pulse-channel arguments");
+    return PQD_OK;
+}
+
+int check_grid(const pqd_grid* g) {
+    if (!g) return fail(PQD_ERR_ARG, "grid is NULL");
+    if (g->n_steps < 0) return fail(PQD_ERR_ARG, "n_steps < 0");
+    if (!(g->dt > 0)) return fail(PQD_ERR_ARG, "dt must be > 0");
+    if (g->n_sub < 1 || g->n_sub > 64) return fail(PQD_ERR_ARG, "n_sub %d not in [1, 64]", g->n_sub);
+    return PQD_OK;
+}
+
+struct Generators {
+    std::vector<cd> L0, S, T, samples;
+};
+
+void build_generators(const pqd_system* sys, Generators& G) {
+    const int N = sys->dim, N2 = N * N;
+    const size_t m2 = (size_t)N2 * N2;
+    G.L0.assign(m2, 0.0);
+    commutator(N, C(sys->H0), sys->hbar, G.L0.data());
+    for (int q = 0; q < sys->n_lind; ++q)
+        dissipator(N, C(sys->lind_ops) + (size_t)q * N * N, sys->lind_rates[q], G.L0.data());
+    const int nc = sys->n_chan;
+    G.S.assign(std::max<size_t>(1, nc * m2), 0.0);
+    G.T.assign(std::max<size_t>(1, nc * m2), 0.0);
+    for (int p = 0; p < nc; ++p) {
+        const cd* X = C(sys->chan_ops) + (size_t)p * N * N;
+        std::vector<cd> Xd(N * N);
+        for (int i = 0; i < N; ++i)
+            for (int j = 0; j < N; ++j) Xd[i * N + j] = std::conj(X[j * N + i]);
+        commutator(N, X, sys->hbar, G.S.data() + p * m2);
+        commutator(N, Xd.data(), sys->hbar, G.T.data() + p * m2);
+    }
+    if (nc > 0)
+        G.samples.assign(C(sys->chan_samples), C(sys->chan_samples) + (size_t)nc * sys->n_samples);
+    else
+        G.samples.assign(1, 0.0);
+}
+
+}  // namespace
+
+// =================================================================================================
+struct pqd_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+};
+
+struct pqd_pt {
+    pqd_ctx* ctx = nullptr;
+    int dim = 0, chi = 0, CHI = 0, D = 0, n_slices = 0;
+    DevBuf<double2> Q, closure, closure0, bond0;
+    DevBuf<int> gmap;
+};
+
+struct pqd_plan {
+    pqd_ctx* ctx = nullptr;
+    int N2 = 0, CHI = 1, n_traj = 0, n_blocks = 0, n_steps = 0, n_chan = 0;
+    bool nopt = true;
+    DevBuf<double2> L0, S, T, samples, M, rho0, ovec, sop, out, cl_ones;
+    DevBuf<int> sched, blk_traj, blk_end, wbeg, wend, ev_start;
+    DevBuf<long long> woff;
+    DevBuf<int4> ev;
+    FreePropParams fp{};
+    SweepParams sp{};
+    int64_t out_len = 0;
+    std::vector<hipEvent_t> evs;  // triplets per execute
+    int32_t execs = 0;
+};
+
+extern "C" {
+
+int32_t pqd_version(void) { return 1; }
+const char* pqd_last_error(void) { return g_err.c_str(); }
+
+int pqd_ctx_create(int32_t device, pqd_ctx** out) {
+    if (!out) return fail(PQD_ERR_ARG, "out is NULL");
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(PQD_ERR_ARG, "device %d out of range (%d devices)", device, ndev);
+    HIPCHK(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(PQD_ERR_UNSUPPORTED, "libpqd is built for gfx950 (MI355X); device is %s", prop.gcnArchName);
+    auto* c = new pqd_ctx;
+    c->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return fail(PQD_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
+    }
+    *out = c;
+    return PQD_OK;
+}
+
+void pqd_ctx_destroy(pqd_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int pqd_ctx_synchronize(pqd_ctx* ctx) {
+    if (!ctx) return fail(PQD_ERR_ARG, "ctx is NULL");
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PQD_OK;
+}
+
+int pqd_pt_create(pqd_ctx* ctx, int32_t dim, const pqd_pt_desc* d, pqd_pt** out) {
+    if (!ctx || !d || !out) return fail(PQD_ERR_ARG, "NULL argument");
+    if (dim < 2 || dim > 6) return fail(PQD_ERR_UNSUPPORTED, "dim %d", dim);
+    const int N2 = dim * dim;
+    const int CHI = pad_chi(d->chi);
+    if (d->chi < 1 || CHI < 0) return fail(PQD_ERR_UNSUPPORTED, "chi %d not in [1, 64]", d->chi);
+    if (d->D < 1 || d->n_slices < 1) return fail(PQD_ERR_ARG, "D and n_slices must be >= 1");
+    if (!d->Q || !d->closure || !d->closure0 || !d->bond0 || !d->gmap) return fail(PQD_ERR_ARG, "NULL PT array");
+    for (int a = 0; a < N2; ++a)
+        if (d->gmap[a] < 0 || d->gmap[a] >= d->D) return fail(PQD_ERR_ARG, "gmap[%d]=%d out of [0,%d)", a, d->gmap[a], d->D);
+    HIPCHK(hipSetDevice(ctx->device));
+    const int chi = d->chi;
+    const size_t qn = (size_t)d->n_slices * d->D * CHI * CHI;
+    std::vector<double2> Q(qn, make_double2(0, 0)), cl((size_t)d->n_slices * CHI, make_double2(0, 0));
+    std::vector<double2> c0(CHI, make_double2(0, 0)), b0(CHI, make_double2(0, 0));
+    const double2* src = reinterpret_cast<const double2*>(d->Q);
+    for (size_t s = 0; s < (size_t)d->n_slices * d->D; ++s)
+        for (int r = 0; r < chi; ++r)
+            std::memcpy(&Q[(s * CHI + r) * CHI], &src[(s * chi + r) * chi], sizeof(double2) * chi);
+    for (int s = 0; s < d->n_slices; ++s)
+        std::memcpy(&cl[(size_t)s * CHI], reinterpret_cast<const double2*>(d->closure) + (size_t)s * chi,
+                    sizeof(double2) * chi);
+    std::memcpy(c0.data(), d->closure0, sizeof(double2) * chi);
+    std::memcpy(b0.data(), d->bond0, sizeof(double2) * chi);
+    auto* pt = new pqd_pt;
+    pt->ctx = ctx; pt->dim = dim; pt->chi = chi; pt->CHI = CHI; pt->D = d->D; pt->n_slices = d->n_slices;
+    hipError_t e = pt->Q.upload(Q.data(), qn, ctx->stream);
+    if (e == hipSuccess) e = pt->closure.upload(cl.data(), cl.size(), ctx->stream);
+    if (e == hipSuccess) e = pt->closure0.upload(c0.data(), CHI, ctx->stream);
+    if (e == hipSuccess) e = pt->bond0.upload(b0.data(), CHI, ctx->stream);
+    if (e == hipSuccess) e = pt->gmap.upload(d->gmap, N2, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) {
+        delete pt;
+        return fail(e == hipErrorOutOfMemory ? PQD_ERR_NOMEM : PQD_ERR_HIP, "PT upload: %s", hipGetErrorString(e));
+    }
+    *out = pt;
+    return PQD_OK;
+}
+
+void pqd_pt_destroy(pqd_pt* pt) { delete pt; }
+
+int pqd_free_propagators(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* grid, pqd_c128* M_out) {
+    if (!ctx || !M_out) return fail(PQD_ERR_ARG, "NULL argument");
+    int rc = check_system(sys);
+    if (rc) return rc;
+    if ((rc = check_grid(grid))) return rc;
+    HIPCHK(hipSetDevice(ctx->device));
+    const int N2 = sys->dim * sys->dim;
+    Generators G;
+    build_generators(sys, G);
+    DevBuf<double2> L0, S, T, smp, M;
+    hipStream_t s = ctx->stream;
+    HIPCHK(L0.upload(reinterpret_cast<double2*>(G.L0.data()), G.L0.size(), s));
+    HIPCHK(S.upload(reinterpret_cast<double2*>(G.S.data()), G.S.size(), s));
+    HIPCHK(T.upload(reinterpret_cast<double2*>(G.T.data()), G.T.size(), s));
+    HIPCHK(smp.upload(reinterpret_cast<double2*>(G.samples.data()), G.samples.size(), s));
+    const size_t nM = (size_t)2 * grid->n_steps * N2 * N2;
+    HIPCHK(M.alloc(nM));
+    FreePropParams fp{};
+    fp.L0 = L0.p; fp.S = S.p; fp.T = T.p; fp.samples = smp.p;
+    fp.n_chan = sys->n_chan; fp.n_samples = std::max(1, sys->n_samples);
+    fp.s_t0 = sys->sample_t0; fp.s_dt = sys->n_chan > 0 ? sys->sample_dt : 1.0;
+    fp.ta = grid->ta; fp.dt = grid->dt; fp.n_steps = grid->n_steps; fp.n_sub = grid->n_sub; fp.M = M.p;
+    HIPCHK(launch_free_prop(N2, fp, s));
+    if (nM) HIPCHK(hipMemcpyAsync(M_out, M.p, nM * sizeof(double2), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return PQD_OK;
+}
+
+int pqd_plan_create(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* grid, const pqd_pt* pt,
+                    const int32_t* sched, const pqd_c128* rho0, int32_t n_out, const pqd_c128* out_ops,
+                    const pqd_traj* tr, int64_t out_len, pqd_plan** out) {
+    if (!ctx || !rho0 || !tr || !out) return fail(PQD_ERR_ARG, "NULL argument");
+    int rc = check_system(sys);
+    if (rc) return rc;
+    if ((rc = check_grid(grid))) return rc;
+    const int N = sys->dim, N2 = N * N;
+    const size_t m2 = (size_t)N2 * N2;
+    const int ns = grid->n_steps;
+    if (n_out < 1 || n_out > 256 || !out_ops) return fail(PQD_ERR_ARG, "n_out %d not in [1, 256]", n_out);
+    if (tr->n_traj < 0 || (tr->n_traj > 0 && (!tr->out_begin || !tr->out_end || !tr->out_offset)))
+        return fail(PQD_ERR_ARG, "bad trajectory arrays");
+    if (pt) {
+        if (pt->ctx != ctx) return fail(PQD_ERR_ARG, "PT belongs to another context");
+        if (pt->dim != N) return fail(PQD_ERR_ARG, "PT dim %d != system dim %d", pt->dim, N);
+        if (!sweep_supported(N2, pt->CHI)) return fail(PQD_ERR_UNSUPPORTED, "N2=%d CHI=%d", N2, pt->CHI);
+    }
+    for (int t = 0; t < tr->n_traj; ++t) {
+        const int b = tr->out_begin[t], e = tr->out_end[t];
+        if (b < 0 || e < b || e > ns)
+            return fail(PQD_ERR_ARG, "trajectory %d window [%d, %d] outside [0, %d]", t, b, e, ns);
+        const int64_t hi = tr->out_offset[t] + (int64_t)(e - b + 1) * n_out;
+        if (tr->out_offset[t] < 0 || hi > out_len)
+            return fail(PQD_ERR_ARG, "trajectory %d output [%lld, %lld) exceeds out_len %lld", t,
+                        (long long)tr->out_offset[t], (long long)hi, (long long)out_len);
+    }
+    if (tr->n_mto < 0 || (tr->n_mto > 0 && (!tr->mto_traj || !tr->mto_step || !tr->mto_before || !tr->mto_kind || !tr->mto_ops)))
+        return fail(PQD_ERR_ARG, "bad MTO arrays");
+    for (int q = 0; q < tr->n_mto; ++q) {
+        if (tr->mto_traj[q] < 0 || tr->mto_traj[q] >= tr->n_traj) return fail(PQD_ERR_ARG, "MTO %d: bad trajectory", q);
+        if (tr->mto_step[q] < 0 || tr->mto_step[q] > ns) return fail(PQD_ERR_ARG, "MTO %d: step %d outside [0, %d]", q, tr->mto_step[q], ns);
+        if (tr->mto_kind[q] < 0 || tr->mto_kind[q] > 2) return fail(PQD_ERR_ARG, "MTO %d: kind %d", q, tr->mto_kind[q]);
+    }
+    std::vector<int32_t> sch(std::max(1, ns), 0);
+    if (pt) {
+        for (int n = 0; n < ns; ++n) {
+            const int s = sched ? sched[n] : std::min(n, pt->n_slices - 1);
+            if (s < 0 || s >= pt->n_slices) return fail(PQD_ERR_ARG, "sched[%d]=%d out of [0,%d)", n, s, pt->n_slices);
+            sch[n] = s;
+        }
+    }
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    auto* P = new pqd_plan;
+    std::unique_ptr<pqd_plan> guard(P);
+    P->ctx = ctx; P->N2 = N2; P->n_traj = tr->n_traj; P->n_steps = ns; P->out_len = out_len;
+    P->nopt = (pt == nullptr);
+    P->CHI = pt ? pt->CHI : 1;
+    P->n_chan = sys->n_chan;
+
+    // ---- generators for the free propagators
+    Generators G;
+    build_generators(sys, G);
+    HIPCHK(P->L0.upload(reinterpret_cast<double2*>(G.L0.data()), G.L0.size(), s));
+    HIPCHK(P->S.upload(reinterpret_cast<double2*>(G.S.data()), G.S.size(), s));
+    HIPCHK(P->T.upload(reinterpret_cast<double2*>(G.T.data()), G.T.size(), s));
+    HIPCHK(P->samples.upload(reinterpret_cast<double2*>(G.samples.data()), G.samples.size(), s));
+    HIPCHK(P->M.alloc(std::max<size_t>(1, (size_t)2 * ns * m2)));
+
+    // ---- MTO events: per trajectory, stable-sorted by (step, phase), same-slot ops composed
+    std::vector<std::vector<int>> per(tr->n_traj);
+    for (int q = 0; q < tr->n_mto; ++q) per[tr->mto_traj[q]].push_back(q);
+    std::vector<int> ev_start(tr->n_traj + 1, 0);
+    std::vector<int4> evs;
+    std::vector<cd> sops;
+    std::vector<cd> tmpS(m2), acc(m2);
+    for (int t = 0; t < tr->n_traj; ++t) {
+        auto& v = per[t];
+        auto key = [&](int q) { return 2 * tr->mto_step[q] + (tr->mto_before[q] ? 0 : 1); };
+        std::stable_sort(v.begin(), v.end(), [&](int a, int b) { return key(a) < key(b); });
+        ev_start[t] = (int)evs.size();
+        size_t i = 0;
+        while (i < v.size()) {
+            const int k0 = key(v[i]);
+            bool first = true;
+            for (; i < v.size() && key(v[i]) == k0; ++i) {
+                const int q = v[i];
+                mto_superop(N, tr->mto_kind[q], C(tr->mto_ops) + (size_t)q * N * N, tmpS.data());
+                if (first) { acc = tmpS; first = false; }
+                else matmul_sq(N2, tmpS.data(), acc.data(), acc.data());
+            }
+            const int idx = (int)(sops.size() / m2);
+            sops.insert(sops.end(), acc.begin(), acc.end());
+            evs.push_back(make_int4(k0 >> 1, k0 & 1, idx, 0));
+        }
+    }
+    ev_start[tr->n_traj] = (int)evs.size();
+    if (evs.empty()) evs.push_back(make_int4(-1, -1, 0, 0));
+    if (sops.empty()) sops.assign(m2, 0.0);
+    HIPCHK(P->ev.upload(evs.data(), evs.size(), s));
+    HIPCHK(P->ev_start.upload(ev_start.data(), ev_start.size(), s));
+    HIPCHK(P->sop.upload(reinterpret_cast<double2*>(sops.data()), sops.size(), s));
+
+    // ---- output operators: ovec[k][i*N+j] = O_k[j][i]   (<O> = Tr(O rho))
+    std::vector<cd> ov((size_t)n_out * N2);
+    for (int k = 0; k < n_out; ++k)
+        for (int i = 0; i < N; ++i)
+            for (int j = 0; j < N; ++j) ov[(size_t)k * N2 + i * N + j] = C(out_ops)[(size_t)k * N2 + j * N + i];
+    HIPCHK(P->ovec.upload(reinterpret_cast<double2*>(ov.data()), ov.size(), s));
+    HIPCHK(P->rho0.upload(reinterpret_cast<const double2*>(rho0), N2, s));
+
+    // ---- trajectory windows and block grouping (longest first so lock-step blocks end together)
+    HIPCHK(P->wbeg.upload(tr->out_begin, std::max(1, tr->n_traj), s));
+    HIPCHK(P->wend.upload(tr->out_end, std::max(1, tr->n_traj), s));
+    HIPCHK(P->woff.upload(reinterpret_cast<const long long*>(tr->out_offset), std::max(1, tr->n_traj), s));
+    std::vector<int> order(tr->n_traj);
+    for (int t = 0; t < tr->n_traj; ++t) order[t] = t;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return tr->out_end[a] > tr->out_end[b]; });
+    const int nb = (tr->n_traj + 3) / 4;
+    std::vector<int> bt(std::max(1, nb * 4), -1), be(std::max(1, nb), 0);
+    for (int k = 0; k < tr->n_traj; ++k) {
+        bt[k] = order[k];
+        be[k / 4] = std::max(be[k / 4], tr->out_end[order[k]]);
+    }
+    P->n_blocks = nb;
+    HIPCHK(P->blk_traj.upload(bt.data(), bt.size(), s));
+    HIPCHK(P->blk_end.upload(be.data(), be.size(), s));
+    HIPCHK(P->sched.upload(sch.data(), sch.size(), s));
+    HIPCHK(P->out.alloc(std::max<int64_t>(1, out_len)));
+    HIPCHK(hipMemsetAsync(P->out.p, 0, std::max<int64_t>(1, out_len) * sizeof(double2), s));
+
+    P->fp.L0 = P->L0.p; P->fp.S = P->S.p; P->fp.T = P->T.p; P->fp.samples = P->samples.p;
+    P->fp.n_chan = sys->n_chan; P->fp.n_samples = std::max(1, sys->n_samples);
+    P->fp.s_t0 = sys->sample_t0; P->fp.s_dt = sys->n_chan > 0 ? sys->sample_dt : 1.0;
+    P->fp.ta = grid->ta; P->fp.dt = grid->dt; P->fp.n_steps = ns; P->fp.n_sub = grid->n_sub; P->fp.M = P->M.p;
+
+    SweepParams& sp = P->sp;
+    sp.M = P->M.p;
+    if (pt) {
+        sp.Q = pt->Q.p; sp.D = pt->D; sp.closure = pt->closure.p; sp.closure0 = pt->closure0.p;
+        sp.bond0 = pt->bond0.p; sp.gmap = pt->gmap.p;
+    }
+    sp.sched = P->sched.p; sp.rho0 = P->rho0.p; sp.n_out = n_out; sp.ovec = P->ovec.p;
+    sp.blk_traj = P->blk_traj.p; sp.blk_end = P->blk_end.p; sp.wbeg = P->wbeg.p; sp.wend = P->wend.p;
+    sp.woff = P->woff.p; sp.ev_start = P->ev_start.p; sp.ev = P->ev.p; sp.sop = P->sop.p; sp.out = P->out.p;
+    HIPCHK(hipStreamSynchronize(s));
+    *out = guard.release();
+    return PQD_OK;
+}
+
+int pqd_plan_execute(pqd_plan* P, int32_t rebuild_free) {
+    if (!P) return fail(PQD_ERR_ARG, "plan is NULL");
+    HIPCHK(hipSetDevice(P->ctx->device));
+    hipStream_t s = P->ctx->stream;
+    hipEvent_t e[3];
+    for (int i = 0; i < 3; ++i) HIPCHK(hipEventCreate(&e[i]));
+    HIPCHK(hipEventRecord(e[0], s));
+    if (rebuild_free && P->n_steps > 0) HIPCHK(launch_free_prop(P->N2, P->fp, s));
+    HIPCHK(hipEventRecord(e[1], s));
+    if (P->nopt)
+        HIPCHK(launch_sweep_nopt(P->N2, P->n_traj, P->sp, s));
+    else
+        HIPCHK(launch_sweep(P->N2, P->CHI, P->n_blocks, P->sp, s));
+    HIPCHK(hipEventRecord(e[2], s));
+    for (int i = 0; i < 3; ++i) P->evs.push_back(e[i]);
+    P->execs++;
+    return PQD_OK;
+}
+
+void* pqd_plan_output_device(pqd_plan* P) { return P ? (void*)P->out.p : nullptr; }
+
+int pqd_plan_download(pqd_plan* P, pqd_c128* out, int64_t out_len) {
+    if (!P || !out) return fail(PQD_ERR_ARG, "NULL argument");
+    if (out_len < P->out_len) return fail(PQD_ERR_ARG, "out_len %lld < plan out_len %lld", (long long)out_len, (long long)P->out_len);
+    HIPCHK(hipSetDevice(P->ctx->device));
+    if (P->out_len > 0)
+        HIPCHK(hipMemcpyAsync(out, P->out.p, P->out_len * sizeof(double2), hipMemcpyDeviceToHost, P->ctx->stream));
+    HIPCHK(hipStreamSynchronize(P->ctx->stream));
+    return PQD_OK;
+}
+
+int pqd_plan_timing(pqd_plan* P, double* ms_free, double* ms_sweep, int32_t* n, int32_t reset) {
+    if (!P) return fail(PQD_ERR_ARG, "plan is NULL");
+    HIPCHK(hipSetDevice(P->ctx->device));
+    double f = 0, w = 0;
+    const int k = (int)P->evs.size() / 3;
+    for (int i = 0; i < k; ++i) {
+        float a = 0, b = 0;
+        HIPCHK(hipEventSynchronize(P->evs[3 * i + 2]));
+        HIPCHK(hipEventElapsedTime(&a, P->evs[3 * i], P->evs[3 * i + 1]));
+        HIPCHK(hipEventElapsedTime(&b, P->evs[3 * i + 1], P->evs[3 * i + 2]));
+        f += a; w += b;
+    }
+    if (ms_free) *ms_free = k ? f / k : 0.0;
+    if (ms_sweep) *ms_sweep = k ? w / k : 0.0;
+    if (n) *n = k;
+    if (reset) {
+        for (auto ev : P->evs) (void)hipEventDestroy(ev);
+        P->evs.clear();
+    }
+    return PQD_OK;
+}
+
+void pqd_plan_destroy(pqd_plan* P) {
+    if (!P) return;
+    (void)hipSetDevice(P->ctx->device);
+    (void)hipStreamSynchronize(P->ctx->stream);
+    for (auto ev : P->evs) (void)hipEventDestroy(ev);
+    delete P;
+}
+
+int pqd_propagate(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* grid, const pqd_pt* pt,
+                  const int32_t* sched, const pqd_c128* rho0, int32_t n_out, const pqd_c128* out_ops,
+                  const pqd_traj* tr, pqd_c128* out, int64_t out_len) {
+    pqd_plan* P = nullptr;
+    int rc = pqd_plan_create(ctx, sys, grid, pt, sched, rho0, n_out, out_ops, tr, out_len, &P);
+    if (rc) return rc;
+    rc = pqd_plan_execute(P, 1);
+    if (!rc) rc = pqd_plan_download(P, out, out_len);
+    pqd_plan_destroy(P);
+    return rc;
+}
+
+// =================================================================================================
+// map-chain sweeps
+// =================================================================================================
+static int mapchain_run(pqd_ctx* ctx, MapChainParams& p, const pqd_c128* dmA, size_t nA, const pqd_c128* dmB,
+                        size_t nB, const pqd_c128* dmT, size_t nT, const pqd_c128* dm_s, const pqd_c128* rho_init,
+                        const pqd_c128* opA, const pqd_c128* opB, const pqd_c128* opC, const double* time,
+                        const double* time_sparse, pqd_c128* result) {
+    if (!ctx || !rho_init || !opA || !opB || !opC || !time || !time_sparse || !result || !dmA)
+        return fail(PQD_ERR_ARG, "NULL argument");
+    if (p.dim < 2 || p.dim > 6) return fail(PQD_ERR_UNSUPPORTED, "dim %d not in [2, 6]", p.dim);
+    if (p.n_t < 1 || p.n_tfull < 1 || p.n_tau < 0) return fail(PQD_ERR_ARG, "bad sizes");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const int N2 = p.dim * p.dim;
+    p.N2 = N2;
+    const size_t m2 = (size_t)N2 * N2;
+    DevBuf<double2> A, Bm, Tm, Ds, r0, oa, ob, oc, rb, res;
+    DevBuf<double> tm, ts;
+    DevBuf<int> ja;
+    auto up = [&](DevBuf<double2>& b, const pqd_c128* src, size_t n) {
+        return b.upload(reinterpret_cast<const double2*>(src), n, s);
+    };
+    HIPCHK(up(A, dmA, nA * m2));
+    if (dmB) HIPCHK(up(Bm, dmB, nB * m2));
+    if (dmT) HIPCHK(up(Tm, dmT, nT * m2));
+    if (dm_s) HIPCHK(up(Ds, dm_s, m2));
+    HIPCHK(up(r0, rho_init, N2));
+    HIPCHK(up(oa, opA, N2));
+    HIPCHK(up(ob, opB, N2));
+    HIPCHK(up(oc, opC, N2));
+    HIPCHK(tm.upload(time, p.n_tfull, s));
+    HIPCHK(ts.upload(time_sparse, p.n_t, s));
+    HIPCHK(rb.alloc((size_t)p.n_t * N2));
+    HIPCHK(ja.alloc(p.n_t));
+    const size_t nres = (size_t)p.n_t * (p.n_tau + 1);
+    HIPCHK(res.alloc(nres));
+    HIPCHK(hipMemsetAsync(res.p, 0, nres * sizeof(double2), s));
+    p.dmA = A.p; p.dmB = Bm.p; p.dmT = Tm.p; p.dm_s = Ds.p; p.rho_init = r0.p;
+    p.opA = oa.p; p.opB = ob.p; p.opC = oc.p; p.time = tm.p; p.time_sparse = ts.p;
+    p.rho_buf = rb.p; p.j_arr = ja.p; p.result = res.p;
+    HIPCHK(launch_mapchain(p, s));
+    HIPCHK(hipMemcpyAsync(result, res.p, nres * sizeof(double2), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return PQD_OK;
+}
+
+int pqd_calc_onetime_parallel(pqd_ctx* ctx, const pqd_c128* dm_tl, const pqd_c128* rho_init, int32_t n_tau,
+                              int32_t n_t, int32_t n_tfull, int32_t dim, const pqd_c128* opA,
+                              const pqd_c128* opB, const pqd_c128* opC, const double* time,
+                              const double* time_sparse, pqd_c128* result) {
+    MapChainParams p{};
+    p.mode = 0; p.dim = dim; p.n_t = n_t; p.n_tfull = n_tfull; p.n_tau = n_tau;
+    // the tau loop reads maps up to index j_max - 1 + n_tau <= n_tfull - 1 (Fortran bounds)
+    return mapchain_run(ctx, p, dm_tl, (size_t)std::max(1, n_tfull - 1), nullptr, 0, nullptr, 0, nullptr, rho_init,
+                        opA, opB, opC, time, time_sparse, result);
+}
+
+int pqd_calc_onetime_parallel_block(pqd_ctx* ctx, const pqd_c128* dm_block, const pqd_c128* dm_s,
+                                    const pqd_c128* rho_init, int32_t n_tb, int32_t nx_tau, int32_t n_map,
+                                    int32_t n_t, int32_t n_tfull, int32_t dim, const pqd_c128* opA,
+                                    const pqd_c128* opB, const pqd_c128* opC, const double* time,
+                                    const double* time_sparse, pqd_c128* result) {
+    if (!dm_s) return fail(PQD_ERR_ARG, "dm_s is NULL");
+    if (n_map < 1 || n_tb < 1 || nx_tau < 0) return fail(PQD_ERR_ARG, "bad block sizes");
+    MapChainParams p{};
+    p.mode = 1; p.dim = dim; p.n_t = n_t; p.n_tfull = n_tfull; p.n_tau = n_tb * nx_tau;
+    p.n_map = n_map; p.n_tb = n_tb; p.nx_tau = nx_tau;
+    return mapchain_run(ctx, p, dm_block, n_map, nullptr, 0, nullptr, 0, dm_s, rho_init, opA, opB, opC, time,
+                        time_sparse, result);
+}
+
+int pqd_calc_twotime_phonon_block(pqd_ctx* ctx, const pqd_c128* dm_taucs2, const pqd_c128* dm_sep1,
+                                  const pqd_c128* dm_sep2, const pqd_c128* dm_s, const pqd_c128* rho_init,
+                                  int32_t n_tb, int32_t nx_tau, int32_t n_map, int32_t n_t, int32_t n_tfull,
+                                  int32_t n_tauc, int32_t dim, const pqd_c128* opA, const pqd_c128* opB,
+                                  const pqd_c128* opC, const double* time, const double* time_sparse,
+                                  pqd_c128* result) {
+    if (!dm_taucs2 || !dm_sep2 || !dm_s) return fail(PQD_ERR_ARG, "NULL map argument");
+    if (n_map < 1 || n_tb < 1 || nx_tau < 0 || n_tauc < 0) return fail(PQD_ERR_ARG, "bad block sizes");
+    if (n_tauc > n_t) return fail(PQD_ERR_ARG, "n_tauc %d > n_t %d (reads past rho_buffer in the reference)", n_tauc, n_t);
+    MapChainParams p{};
+    p.mode = 2; p.dim = dim; p.n_t = n_t; p.n_tfull = n_tfull; p.n_tau = n_tb * nx_tau;
+    p.n_map = n_map; p.n_tb = n_tb; p.nx_tau = nx_tau; p.n_tauc = n_tauc;
+    return mapchain_run(ctx, p, dm_sep1, n_map, dm_sep2, n_map, dm_taucs2, (size_t)std::max(1, n_tauc) * n_map, dm_s,
+                        rho_init, opA, opB, opC, time, time_sparse, result);
+}
+
+int pqd_propagate_tau(pqd_ctx* ctx, const pqd_c128* dm_tl, int32_t n_maps, const pqd_c128* rho_init,
+                      int32_t n_tau, int32_t dim, int32_t j_start, pqd_c128* rho_out) {
+    if (!ctx || !dm_tl || !rho_init || !rho_out) return fail(PQD_ERR_ARG, "NULL argument");
+    if (dim < 2 || dim > 6) return fail(PQD_ERR_UNSUPPORTED, "dim %d", dim);
+    if (n_tau < 0 || j_start < 0 || j_start + n_tau > n_maps)
+        return fail(PQD_ERR_ARG, "maps j_start+1..j_start+n_tau = %d..%d outside 1..%d", j_start + 1, j_start + n_tau, n_maps);
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const int N2 = dim * dim;
+    DevBuf<double2> A, r0, o;
+    HIPCHK(A.upload(reinterpret_cast<const double2*>(dm_tl), (size_t)n_maps * N2 * N2, s));
+    HIPCHK(r0.upload(reinterpret_cast<const double2*>(rho_init), N2, s));
+    HIPCHK(o.alloc((size_t)N2 * (n_tau + 1)));
+    HIPCHK(launch_propagate_tau(N2, A.p, r0.p, n_tau, j_start, o.p, s));
+    HIPCHK(hipMemcpyAsync(rho_out, o.p, (size_t)N2 * (n_tau + 1) * sizeof(double2), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return PQD_OK;
+}
+
+static int four_time_common(pqd_ctx* ctx, FourTimeParams& p, const pqd_c128* dm_1, const pqd_c128* dm_2,
+                            const pqd_c128* rho_init, const double* t1, const pqd_c128* precalc, const pqd_c128* ops,
+                            int n_ops, pqd_c128* result, bool dyn) {
+    if (!ctx || !dm_1 || !dm_2 || !rho_init || !t1 || !precalc || !result || (!dyn && !ops))
+        return fail(PQD_ERR_ARG, "NULL argument");
+    if (p.dim < 2 || p.dim > 6) return fail(PQD_ERR_UNSUPPORTED, "dim %d", p.dim);
+    if (p.n_t < 1 || p.n_map < 1 || p.n_precalc < 1 || !(p.dt > 0)) return fail(PQD_ERR_ARG, "bad sizes");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const int N2 = p.dim * p.dim;
+    p.N2 = N2;
+    const size_t m2 = (size_t)N2 * N2;
+    DevBuf<double2> d1, d2, pc, r0, op, res;
+    DevBuf<double> tt;
+    DevBuf<int2> pr;
+    HIPCHK(d1.upload(reinterpret_cast<const double2*>(dm_1), p.n_map * m2, s));
+    HIPCHK(d2.upload(reinterpret_cast<const double2*>(dm_2), p.n_map * m2, s));
+    HIPCHK(pc.upload(reinterpret_cast<const double2*>(precalc), p.n_precalc * m2, s));
+    HIPCHK(r0.upload(reinterpret_cast<const double2*>(rho_init), N2, s));
+    HIPCHK(tt.upload(t1, p.n_t, s));
+    if (!dyn) HIPCHK(op.upload(reinterpret_cast<const double2*>(ops), (size_t)n_ops * N2, s));
+    p.dm1 = d1.p; p.dm2 = d2.p; p.precalc = pc.p; p.rho_init = r0.p; p.t1 = tt.p; p.ops = op.p;
+    if (dyn) {
+        const size_t n = (size_t)N2 * (2 * p.n_t - 1);
+        HIPCHK(res.alloc(n));
+        HIPCHK(launch_dynamics_t1(p, res.p, s));
+        HIPCHK(hipMemcpyAsync(result, res.p, n * sizeof(double2), hipMemcpyDeviceToHost, s));
+    } else {
+        std::vector<int2> pairs;
+        pairs.reserve((size_t)p.n_t * (p.n_t + 1) / 2);
+        for (int i = 0; i < p.n_t; ++i)
+            for (int j = 0; j <= p.n_t - 1 - i; ++j) pairs.push_back(make_int2(i, j));
+        HIPCHK(pr.upload(pairs.data(), pairs.size(), s));
+        p.pairs = pr.p; p.n_pairs = (int)pairs.size();
+        const size_t nres = (size_t)p.n_t * p.n_t;
+        HIPCHK(res.alloc(nres + (size_t)p.n_t * N2));  // + prologue scratch
+        HIPCHK(hipMemsetAsync(res.p, 0, nres * sizeof(double2), s));
+        p.result = res.p;
+        HIPCHK(launch_four_time(p, s));
+        HIPCHK(hipMemcpyAsync(result, res.p, nres * sizeof(double2), hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    return PQD_OK;
+}
+
+int pqd_four_time_8op(pqd_ctx* ctx, const pqd_c128* dm_1, const pqd_c128* dm_2, const pqd_c128* rho_init,
+                      const double* t1, const pqd_c128* precalc, int32_t n_t, double dt, int32_t n_map,
+                      int32_t dim, const pqd_c128* ops8, int32_t early_only, int32_t late_t1_only, double tb,
+                      int32_t n_precalc, pqd_c128* result) {
+    FourTimeParams p{};
+    p.dim = dim; p.n_t = n_t; p.n_map = n_map; p.n_precalc = n_precalc; p.dt = dt; p.tb = tb;
+    p.variant = 0; p.early_only = early_only; p.late_t1_only = late_t1_only;
+    return four_time_common(ctx, p, dm_1, dm_2, rho_init, t1, precalc, ops8, 8, result, false);
+}
+
+int pqd_four_time(pqd_ctx* ctx, const pqd_c128* dm_1, const pqd_c128* dm_2, const pqd_c128* rho_init,
+                  const double* t1, const pqd_c128* precalc, int32_t n_t, double dt, int32_t n_map, int32_t dim,
+                  const pqd_c128* ops4, double tb, int32_t n_precalc, pqd_c128* result) {
+    FourTimeParams p{};
+    p.dim = dim; p.n_t = n_t; p.n_map = n_map; p.n_precalc = n_precalc; p.dt = dt; p.tb = tb; p.variant = 1;
+    return four_time_common(ctx, p, dm_1, dm_2, rho_init, t1, precalc, ops4, 4, result, false);
+}
+
+int pqd_dynamics_t1(pqd_ctx* ctx, const pqd_c128* dm_1, const pqd_c128* dm_2, const pqd_c128* rho_init,
+                    const double* t1, const pqd_c128* precalc, int32_t n_t, double dt, int32_t n_map,
+                    int32_t dim, double tb, int32_t n_precalc, pqd_c128* result) {
+    FourTimeParams p{};
+    p.dim = dim; p.n_t = n_t; p.n_map = n_map; p.n_precalc = n_precalc; p.dt = dt; p.tb = tb;
+    return four_time_common(ctx, p, dm_1, dm_2, rho_init, t1, precalc, nullptr, 0, result, true);
+}
+
+}  // extern "C"

@@ -1,0 +1,349 @@
+// pt_sweep.hip — the hot path: lock-step propagation of a batch of trajectories through the
+// process-tensor MPO (PT contraction + symmetric-Trotter free half steps + MTOs + output traces).
+//
+// Replaces the per-step loop inside the external ACE binary that pyaceqd drives through
+// system_ace_stream (general_system.py:227-343) and fans out one OS process per trajectory in the
+// two-time sweeps (two_time/correlations.py:135-184, pol_entanglement/G2.py:439-533, ...).
+//
+// Work decomposition (MI355X: 256 CUs, 160 KiB LDS/CU, 64-wide waves, FP64 VALU = FP64 MFMA peak):
+//   * one 256-thread workgroup owns B = 4 trajectories for the whole time range (persistent over
+//     steps, no inter-workgroup traffic at all: trajectories are independent);
+//   * the 4 augmented states Q_b[alpha][d] (N2 x CHI complex doubles, 16 KiB each at N=4, chi=64)
+//     stay resident in LDS, rows padded to CHI+1 so column reads and row reads are bank-conflict free;
+//   * free half steps (N2 x N2 propagator applied to every bond column): one thread per column (b, d),
+//     the propagator is wave-uniform and streamed through the scalar cache (s_load), the column sits
+//     in VGPRs — no cross-thread traffic, no barrier inside the phase;
+//   * PT contraction (row alpha of all 4 trajectories times the chi x chi slice Q[g(alpha)]): waves
+//     split the alpha rows; lane (j, q) owns output columns {j, j+16, j+32, j+48} and the input
+//     quarter d = 4k + q, so every Q element is read from L2 exactly once per workgroup and feeds
+//     4 trajectories (B) from registers; the 4 quarter partial sums are combined by a 2-stage
+//     reduce-scatter over lanes (xor 16, xor 32);
+//   * closure + output traces only on steps inside some trajectory's output window.
+// All PT slices / free propagators are shared by every workgroup at the same absolute step, so the
+// dominant traffic is L2/MALL-resident; the kernel is FP64-FMA bound at B = 4.
+#include "pqd_common.h"
+#include <climits>
+
+namespace {
+
+constexpr int BT = 4;  // trajectories per workgroup
+
+template <int N2, int CHI>
+struct SweepLayout {
+    static constexpr int RS = CHI + 1;          // row stride (double2)
+    static constexpr int TS = N2 * RS + 4;      // trajectory stride (+64 B: shifts banks per trajectory)
+    static constexpr int KD = CHI / 16;         // PT output columns per lane
+    static constexpr int NCOL = BT * CHI;       // column-phase work items
+    static constexpr size_t LDS = (size_t)(BT * TS + BT * N2) * sizeof(double2);
+};
+
+// column op: col <- Op col   (Op row-major N2 x N2; result written straight back to the LDS column)
+template <int N2, int RS>
+__device__ __forceinline__ void col_apply(const double2* __restrict__ Op, double2* col) {
+    double2 v[N2];
+#pragma unroll
+    for (int a = 0; a < N2; ++a) v[a] = col[a * RS];
+    for (int r = 0; r < N2; ++r) {
+        const double2* Or = Op + r * N2;
+        double2 acc = c_zero();
+#pragma unroll
+        for (int a = 0; a < N2; ++a) c_fma(acc, Or[a], v[a]);
+        col[r * RS] = acc;
+    }
+}
+
+template <int N2, int CHI>
+__global__ __launch_bounds__(256) void pt_sweep_kernel(SweepParams p) {
+    using L = SweepLayout<N2, CHI>;
+    constexpr int RS = L::RS, TS = L::TS, KD = L::KD, NCOL = L::NCOL;
+    extern __shared__ __attribute__((aligned(16))) double2 smem[];
+    double2* st = smem;
+    double2* rbuf = smem + BT * TS;
+    __shared__ int s_traj[BT], s_wb[BT], s_we[BT];
+    __shared__ long long s_wo[BT];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    if (tid < BT) {
+        const int t = p.blk_traj[blockIdx.x * BT + tid];
+        s_traj[tid] = t;
+        s_wb[tid] = t >= 0 ? p.wbeg[t] : INT_MAX;
+        s_we[tid] = t >= 0 ? p.wend[t] : -1;
+        s_wo[tid] = t >= 0 ? p.woff[t] : 0;
+    }
+    __syncthreads();
+    const int n_end = p.blk_end[blockIdx.x];
+
+    // ---- column-phase ownership: thread -> column (cb, cd)
+    const bool colthr = tid < NCOL;
+    const int cb = tid / CHI, cd = tid - (tid / CHI) * CHI;
+    double2* col = st + cb * TS + cd;
+    int ev_cur = 0, ev_lim = 0;
+    if (colthr) {
+        const int t = s_traj[cb];
+        if (t >= 0) { ev_cur = p.ev_start[t]; ev_lim = p.ev_start[t + 1]; }
+        const double2 b0 = p.bond0[cd];
+#pragma unroll
+        for (int a = 0; a < N2; ++a) col[a * RS] = c_mul(p.rho0[a], b0);
+        while (ev_cur < ev_lim) {  // applyBefore-true MTOs at step 0
+            const int4 e = p.ev[ev_cur];
+            if (e.x != 0 || e.y != 0) break;
+            col_apply<N2, RS>(p.sop + (size_t)e.z * N2 * N2, col);
+            ++ev_cur;
+        }
+    }
+    __syncthreads();
+
+    const int pj = lane & 15, pq = lane >> 4;
+    for (int n = 0;; ++n) {
+        // ------------------------------------------------------------ outputs at step n
+        bool need = false;
+#pragma unroll
+        for (int b = 0; b < BT; ++b) need |= (s_wb[b] <= n) & (n <= s_we[b]);
+        if (need) {
+            const double2* cvec = (n == 0) ? p.closure0 : p.closure + (size_t)p.sched[n - 1] * CHI;
+            constexpr int NPART = BT * N2 * 4;
+            for (int it = 0; it < (NPART + 255) / 256; ++it) {
+                const int e = tid + 256 * it;
+                const int row = e >> 2, qr = e & 3;
+                double2 s = c_zero();
+                if (e < NPART) {
+                    const int b = row / N2, a = row - (row / N2) * N2;
+                    const double2* rp = st + b * TS + a * RS + qr;
+#pragma unroll 4
+                    for (int kk = 0; kk < CHI / 4; ++kk) c_fma(s, rp[4 * kk], cvec[4 * kk + qr]);
+                }
+                s = c_add(s, c_shfl_xor(s, 1));
+                s = c_add(s, c_shfl_xor(s, 2));
+                if (e < NPART && qr == 0) rbuf[row] = s;
+            }
+            __syncthreads();
+            for (int e = tid; e < BT * p.n_out; e += 256) {
+                const int b = e / p.n_out, k = e - (e / p.n_out) * p.n_out;
+                if (s_wb[b] <= n && n <= s_we[b]) {
+                    double2 s = c_zero();
+                    const double2* ov = p.ovec + (size_t)k * N2;
+                    for (int a = 0; a < N2; ++a) c_fma(s, ov[a], rbuf[b * N2 + a]);
+                    p.out[s_wo[b] + (long long)(n - s_wb[b]) * p.n_out + k] = s;
+                }
+            }
+        }
+        if (n >= n_end) break;
+
+        // ------------------------------------------------------------ column phase A
+        const double2* Ma = p.M + (size_t)(2 * n) * N2 * N2;
+        if (colthr) {
+            while (ev_cur < ev_lim) {  // applyBefore-false MTOs at step n
+                const int4 e = p.ev[ev_cur];
+                if (e.x != n || e.y != 1) break;
+                col_apply<N2, RS>(p.sop + (size_t)e.z * N2 * N2, col);
+                ++ev_cur;
+            }
+            col_apply<N2, RS>(Ma, col);
+        }
+        __syncthreads();
+
+        // ------------------------------------------------------------ PT contraction
+        {
+            const double2* Qs = p.Q + (size_t)p.sched[n] * p.D * CHI * CHI;
+            for (int a = wave; a < N2; a += 4) {
+                const double2* Qg = Qs + (size_t)p.gmap[a] * CHI * CHI + pj;
+                const double2* xr = st + a * RS + pq;
+                double2 acc[BT][KD];
+#pragma unroll
+                for (int b = 0; b < BT; ++b)
+#pragma unroll
+                    for (int i = 0; i < KD; ++i) acc[b][i] = c_zero();
+                double2 qn[KD];
+#pragma unroll
+                for (int i = 0; i < KD; ++i) qn[i] = Qg[(size_t)pq * CHI + 16 * i];
+#pragma unroll 2
+                for (int kk = 0; kk < CHI / 4; ++kk) {
+                    double2 qv[KD];
+#pragma unroll
+                    for (int i = 0; i < KD; ++i) qv[i] = qn[i];
+                    if (kk + 1 < CHI / 4) {
+                        const int dn = 4 * (kk + 1) + pq;
+#pragma unroll
+                        for (int i = 0; i < KD; ++i) qn[i] = Qg[(size_t)dn * CHI + 16 * i];
+                    }
+#pragma unroll
+                    for (int b = 0; b < BT; ++b) {
+                        const double2 x = xr[b * TS + 4 * kk];
+#pragma unroll
+                        for (int i = 0; i < KD; ++i) c_fma(acc[b][i], x, qv[i]);
+                    }
+                }
+                // reduce the 4 input quarters (lanes j, j+16, j+32, j+48) and scatter the columns
+                double2* wr = st + a * RS + pj;
+                if constexpr (KD == 4) {
+                    const bool q0 = pq & 1, q1 = (pq >> 1) & 1;
+#pragma unroll
+                    for (int b = 0; b < BT; ++b) {
+                        double2 h[2];
+#pragma unroll
+                        for (int pi = 0; pi < 2; ++pi) {
+                            const double2 mine = q0 ? acc[b][2 * pi + 1] : acc[b][2 * pi];
+                            const double2 oth = q0 ? acc[b][2 * pi] : acc[b][2 * pi + 1];
+                            h[pi] = c_add(mine, c_shfl_xor(oth, 16));
+                        }
+                        const double2 mine = q1 ? h[1] : h[0];
+                        const double2 oth = q1 ? h[0] : h[1];
+                        wr[b * TS + 16 * pq] = c_add(mine, c_shfl_xor(oth, 32));
+                    }
+                } else if constexpr (KD == 2) {
+                    const bool q0 = pq & 1;
+#pragma unroll
+                    for (int b = 0; b < BT; ++b) {
+                        const double2 mine = q0 ? acc[b][1] : acc[b][0];
+                        const double2 oth = q0 ? acc[b][0] : acc[b][1];
+                        double2 h = c_add(mine, c_shfl_xor(oth, 16));
+                        h = c_add(h, c_shfl_xor(h, 32));
+                        if (pq < 2) wr[b * TS + 16 * pq] = h;
+                    }
+                } else {
+#pragma unroll
+                    for (int b = 0; b < BT; ++b) {
+                        double2 h = c_add(acc[b][0], c_shfl_xor(acc[b][0], 16));
+                        h = c_add(h, c_shfl_xor(h, 32));
+                        if (pq == 0) wr[b * TS] = h;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+
+        // ------------------------------------------------------------ column phase B
+        const double2* Mb = Ma + N2 * N2;
+        if (colthr) {
+            col_apply<N2, RS>(Mb, col);
+            while (ev_cur < ev_lim) {  // applyBefore-true MTOs at step n+1
+                const int4 e = p.ev[ev_cur];
+                if (e.x != n + 1 || e.y != 0) break;
+                col_apply<N2, RS>(p.sop + (size_t)e.z * N2 * N2, col);
+                ++ev_cur;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// chi = 1 (no environment): one wave per trajectory, lane r owns rho[r]; operators applied through
+// cross-lane shuffles (no LDS, no barriers). Latency-bound by construction (C1: 1 trajectory).
+// ------------------------------------------------------------------------------------------------
+template <int N2>
+__device__ __forceinline__ double2 lane_apply(const double2* __restrict__ Op, double2 own, int lane) {
+    const int r = lane < N2 ? lane : N2 - 1;
+    const double2* Or = Op + r * N2;
+    double2 acc = c_zero();
+#pragma unroll
+    for (int a = 0; a < N2; ++a) {
+        const double2 x = make_double2(__shfl(own.x, a), __shfl(own.y, a));
+        c_fma(acc, Or[a], x);
+    }
+    return acc;
+}
+
+template <int N2>
+__global__ __launch_bounds__(64) void sweep_nopt_kernel(SweepParams p) {
+    const int lane = threadIdx.x;
+    const int t = blockIdx.x;
+    const int wb = p.wbeg[t], we = p.wend[t];
+    const long long wo = p.woff[t];
+    int ev_cur = p.ev_start[t];
+    const int ev_lim = p.ev_start[t + 1];
+    double2 own = lane < N2 ? p.rho0[lane] : c_zero();
+    while (ev_cur < ev_lim) {
+        const int4 e = p.ev[ev_cur];
+        if (e.x != 0 || e.y != 0) break;
+        own = lane_apply<N2>(p.sop + (size_t)e.z * N2 * N2, own, lane);
+        ++ev_cur;
+    }
+    const int k = lane < p.n_out ? lane : p.n_out - 1;
+    for (int n = 0;; ++n) {
+        if (wb <= n && n <= we) {
+            double2 s = c_zero();
+            const double2* ov = p.ovec + (size_t)k * N2;
+#pragma unroll
+            for (int a = 0; a < N2; ++a) {
+                const double2 x = make_double2(__shfl(own.x, a), __shfl(own.y, a));
+                c_fma(s, ov[a], x);
+            }
+            if (lane < p.n_out) p.out[wo + (long long)(n - wb) * p.n_out + lane] = s;
+        }
+        if (n >= we) break;
+        while (ev_cur < ev_lim) {
+            const int4 e = p.ev[ev_cur];
+            if (e.x != n || e.y != 1) break;
+            own = lane_apply<N2>(p.sop + (size_t)e.z * N2 * N2, own, lane);
+            ++ev_cur;
+        }
+        const double2* Ma = p.M + (size_t)(2 * n) * N2 * N2;
+        own = lane_apply<N2>(Ma, own, lane);
+        own = lane_apply<N2>(Ma + N2 * N2, own, lane);
+        while (ev_cur < ev_lim) {
+            const int4 e = p.ev[ev_cur];
+            if (e.x != n + 1 || e.y != 0) break;
+            own = lane_apply<N2>(p.sop + (size_t)e.z * N2 * N2, own, lane);
+            ++ev_cur;
+        }
+    }
+}
+
+template <int N2, int CHI>
+hipError_t launch_sw(int n_blocks, const SweepParams& p, hipStream_t s) {
+    using L = SweepLayout<N2, CHI>;
+    static_assert(L::LDS <= 160 * 1024, "LDS budget");
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)pt_sweep_kernel<N2, CHI>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::LDS);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL((pt_sweep_kernel<N2, CHI>), dim3(n_blocks), dim3(256), L::LDS, s, p);
+    return hipGetLastError();
+}
+
+template <int N2>
+hipError_t launch_sw_chi(int CHI, int n_blocks, const SweepParams& p, hipStream_t s) {
+    switch (CHI) {
+        case 16: return launch_sw<N2, 16>(n_blocks, p, s);
+        case 32: return launch_sw<N2, 32>(n_blocks, p, s);
+        case 64: return launch_sw<N2, 64>(n_blocks, p, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace
+
+bool sweep_supported(int N2, int CHI) {
+    return (N2 == 4 || N2 == 9 || N2 == 16 || N2 == 25 || N2 == 36) &&
+           (CHI == 1 || CHI == 16 || CHI == 32 || CHI == 64);
+}
+
+hipError_t launch_sweep(int N2, int CHI, int n_blocks, const SweepParams& p, hipStream_t s) {
+    if (n_blocks <= 0) return hipSuccess;
+    switch (N2) {
+        case 4: return launch_sw_chi<4>(CHI, n_blocks, p, s);
+        case 9: return launch_sw_chi<9>(CHI, n_blocks, p, s);
+        case 16: return launch_sw_chi<16>(CHI, n_blocks, p, s);
+        case 25: return launch_sw_chi<25>(CHI, n_blocks, p, s);
+        case 36: return launch_sw_chi<36>(CHI, n_blocks, p, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_sweep_nopt(int N2, int n_traj, const SweepParams& p, hipStream_t s) {
+    if (n_traj <= 0) return hipSuccess;
+#define PQD_NOPT(NN) case NN: hipLaunchKernelGGL(sweep_nopt_kernel<NN>, dim3(n_traj), dim3(64), 0, s, p); break;
+    switch (N2) {
+        PQD_NOPT(4) PQD_NOPT(9) PQD_NOPT(16) PQD_NOPT(25) PQD_NOPT(36)
+        default: return hipErrorInvalidValue;
+    }
+#undef PQD_NOPT
+    return hipGetLastError();
+}

@@ -1,0 +1,195 @@
+"""Generate the committed golden fixtures under tests/golden/.
+
+Run in the build container only (needs /root/reference and oracle/_ref built by `make -C oracle ref`):
+    python tests/golden/make_golden.py
+
+Two kinds of vectors, both produced by running the REFERENCE ITSELF on seeded inputs:
+  * fortran_*.npz : outputs of the reference Fortran sweep kernels
+                    (pyaceqd/two_time/propagate_tau.f90, pyaceqd/timebin/timebin_tl.f90), compiled from
+                    their own sources by oracle/Makefile and called through oracle/fref.py.
+  * pyref_*.npz   : outputs of the reference's pure-Python modules that import without ACE
+                    (pyaceqd/pulses.py, pyaceqd/tools.py), imported from /root/reference.
+Inputs are synthetic (numpy default_rng seeds below), stored next to the outputs.
+"""
+import os
+import sys
+
+import numpy as np
+import scipy.linalg as sla
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+from oracle import fref  # noqa: E402
+
+REF_ROOT = "/root/reference"
+
+
+def rand_lindblad_maps(n, dim, h, rng, drift=0.05):
+    """n CPTP maps exp(L_i h) (row-major vec convention) of random Lindbladians that drift with i."""
+    N2 = dim * dim
+    I = np.eye(dim)
+    H = rng.normal(size=(dim, dim)) + 1j * rng.normal(size=(dim, dim)); H = 0.5 * (H + H.conj().T)
+    dH = rng.normal(size=(dim, dim)) + 1j * rng.normal(size=(dim, dim)); dH = 0.5 * (dH + dH.conj().T)
+    Ls = [(rng.normal(size=(dim, dim)) + 1j * rng.normal(size=(dim, dim))) * 0.3 for _ in range(2)]
+    maps = np.empty((n, N2, N2), dtype=np.complex128)
+    for i in range(n):
+        Hi = H + drift * np.sin(0.1 * i) * dH
+        L = -1j * (np.kron(Hi, I) - np.kron(I, Hi.T))
+        for Lk in Ls:
+            LdL = Lk.conj().T @ Lk
+            L = L + np.kron(Lk, Lk.conj()) - 0.5 * np.kron(LdL, I) - 0.5 * np.kron(I, LdL.T)
+        maps[i] = sla.expm(L * h)
+    return maps
+
+
+def rand_op(dim, rng):
+    return rng.normal(size=(dim, dim)) + 1j * rng.normal(size=(dim, dim))
+
+
+def rand_rho(dim, rng):
+    A = rand_op(dim, rng)
+    r = A @ A.conj().T
+    return r / np.trace(r)
+
+
+def F(maps):
+    """(n, N2, N2) row-major stack -> Fortran (N2, N2, n) layout as the reference callers build it
+    (correlations.py:781 `np.asfortranarray(dm_tl.transpose(1, 2, 0))`)."""
+    return np.asfortranarray(maps.transpose(1, 2, 0))
+
+
+def gen_fortran():
+    out = {}
+    for dim in (2, 4, 6):
+        rng = np.random.default_rng(1000 + dim)
+        N2 = dim * dim
+        # --- propagate_tau (propagate_tau.f90:3)
+        maps = rand_lindblad_maps(60, dim, 0.1, rng)
+        rho0 = rand_rho(dim, rng).reshape(N2)
+        n_tau, j_start = 25, 7
+        r = fref.propagate_tau(F(maps), rho0, n_tau, dim, j_start)
+        np.savez_compressed(os.path.join(HERE, f"fortran_propagate_tau_d{dim}.npz"),
+                            dm_tl=maps, rho_init=rho0, n_tau=n_tau, j_start=j_start, rho_out=np.asarray(r))
+        # --- calc_onetime_parallel (propagate_tau.f90:110): time grid + sparse grid incl. off-grid values
+        n_tfull = 90
+        dt = 0.1
+        time = np.round(np.arange(n_tfull) * dt, 6)
+        time_sparse = np.array([0.0, 0.1, 0.25, 0.5, 1.0, 1.05, 2.3, 3.0, 4.4])
+        n_tau = 40
+        opa, opb, opc = rand_op(dim, rng), rand_op(dim, rng), rand_op(dim, rng)
+        maps = rand_lindblad_maps(n_tfull - 1, dim, dt, rng)
+        res = fref.calc_onetime_parallel(F(maps), rho0, n_tau, dim, opa, opb, opc, time, time_sparse)
+        np.savez_compressed(os.path.join(HERE, f"fortran_onetime_d{dim}.npz"),
+                            dm_tl=maps, rho_init=rho0, n_tau=n_tau, opa=opa, opb=opb, opc=opc,
+                            time=time, time_sparse=time_sparse, result=np.asarray(res))
+        # --- calc_onetime_parallel_block (propagate_tau.f90:189)
+        n_map, n_tb, nx_tau = 6, 10, 3
+        dm_block = rand_lindblad_maps(n_map, dim, dt, rng)
+        dm_s = rand_lindblad_maps(1, dim, dt, rng)[0]
+        time_sparse_b = np.array([0.0, 0.2, 0.35, 0.9, 1.5])
+        res = fref.calc_onetime_parallel_block(F(dm_block), dm_s, rho0, n_tb, nx_tau, dim, opa, opb, opc,
+                                               time, time_sparse_b)
+        np.savez_compressed(os.path.join(HERE, f"fortran_onetime_block_d{dim}.npz"),
+                            dm_block=dm_block, dm_s=dm_s, rho_init=rho0, n_tb=n_tb, nx_tau=nx_tau,
+                            opa=opa, opb=opb, opc=opc, time=time, time_sparse=time_sparse_b, result=np.asarray(res))
+        # --- calc_twotime_phonon_block (propagate_tau.f90:374)
+        n_tauc = 3
+        dm_sep1 = rand_lindblad_maps(n_map, dim, dt, rng)
+        dm_sep2 = rand_lindblad_maps(n_map, dim, dt, rng)
+        dm_tc = np.stack([rand_lindblad_maps(n_map, dim, dt, rng) for _ in range(n_tauc)])  # (n_tauc, n_map, N2, N2)
+        dm_taucs2_f = np.asfortranarray(dm_tc.transpose(2, 3, 0, 1))  # purity.py:581
+        time_sparse_p = np.array([0.0, 0.1, 0.2, 0.45, 0.7, 1.2])
+        res = fref.calc_twotime_phonon_block(dm_taucs2_f, F(dm_sep1), F(dm_sep2), dm_s, rho0, n_tb, nx_tau, dim,
+                                             opa, opb, opc, time, time_sparse_p)
+        np.savez_compressed(os.path.join(HERE, f"fortran_twotime_phonon_block_d{dim}.npz"),
+                            dm_taucs2=dm_tc, dm_sep1=dm_sep1, dm_sep2=dm_sep2, dm_s=dm_s, rho_init=rho0,
+                            n_tb=n_tb, nx_tau=nx_tau, opa=opa, opb=opb, opc=opc, time=time,
+                            time_sparse=time_sparse_p, result=np.asarray(res))
+    # --- timebin_tl (timebin_tl.f90): dim 2 and 4 (dim 5 is the reference default, twophoton_new.py:19)
+    for dim in (2, 4, 5):
+        rng = np.random.default_rng(2000 + dim)
+        N2 = dim * dim
+        dt, tb = 0.1, 3.0
+        n_map = 12
+        dm_1 = rand_lindblad_maps(n_map, dim, dt, rng)
+        dm_2 = rand_lindblad_maps(n_map, dim, dt, rng)
+        tl = rand_lindblad_maps(1, dim, dt, rng)[0]
+        n_precalc = int(np.log2(tb / dt)) + 1  # twophoton_new.py:606
+        precalc = np.stack([np.linalg.matrix_power(tl, 2 ** k) for k in range(n_precalc)])
+        # conj-transposed feed as the caller does (twophoton_new.py:114-116)
+        dm_1c = np.conj(dm_1); dm_2c = np.conj(dm_2); prec_c = np.conj(precalc)
+        rho0 = rand_rho(dim, rng).reshape(N2)
+        # non-uniform t1 grid with a value that exercises int(round_to_6(t)/dt) truncation (0.3/0.1 -> 2)
+        t1 = np.array([0.0, 0.1, 0.3, 0.6, 0.7, 1.0, 1.4, 2.0, 2.5])
+        ops8 = [rand_op(dim, rng) for _ in range(8)]
+        res8 = fref.four_time_8op(F(dm_1c), F(dm_2c), rho0, t1, F(prec_c), dt, dim, ops8, False, False, tb)
+        res8e = fref.four_time_8op(F(dm_1c), F(dm_2c), rho0, t1, F(prec_c), dt, dim, ops8, True, False, tb)
+        res8l = fref.four_time_8op(F(dm_1c), F(dm_2c), rho0, t1, F(prec_c), dt, dim, ops8, False, True, tb)
+        res4 = fref.four_time(F(dm_1c), F(dm_2c), rho0, t1, F(prec_c), dt, dim, ops8[0], ops8[1], ops8[2], ops8[3], tb)
+        dyn = fref.dynamics_t1(F(dm_1c), F(dm_2c), rho0, t1, F(prec_c), dt, dim, tb)
+        np.savez_compressed(os.path.join(HERE, f"fortran_timebin_d{dim}.npz"),
+                            dm_1=dm_1c, dm_2=dm_2c, precalc=prec_c, rho_init=rho0, t1=t1, dt=dt, tb=tb,
+                            ops8=np.stack(ops8), result8=np.asarray(res8), result8_early=np.asarray(res8e),
+                            result8_late=np.asarray(res8l), result4=np.asarray(res4), dyn_t1=np.asarray(dyn))
+
+
+def gen_pyref():
+    sys.path.insert(0, REF_ROOT)
+    from pyaceqd import pulses as P  # noqa: E402
+    from pyaceqd import tools as T  # noqa: E402
+    t = np.arange(-10.0, 40.0, 0.05)
+    plist = {
+        "chirped": P.ChirpedPulse(tau_0=3.0, e_start=0.3, alpha=10.0, t0=5.0, e0=1.0, phase=0.2),
+        "chirped_polar": P.ChirpedPulse(tau_0=2.7, e_start=-1.0, alpha=40.0, t0=12.0, e0=5.3, polar_x=0.6),
+        "gauss": P.Pulse(tau=2.0, e_start=0.5, w_gain=0.01, t0=3.0, e0=2.0, phase=0.1),
+        "cw": P.CWLaser(e0=0.05, e_start=0.2),
+        "smooth_rect": P.SmoothRectangle(tau=10.0, e_start=0.1, t0=15.0, e0=0.3, alpha_onoff=0.5),
+        "asym": P.AsymmetricPulse(tau1=2.0, tau2=4.0, e_start=0.0, t0=7.0, e0=1.0),
+    }
+    arrs = {"t": t}
+    for k, p in plist.items():
+        arrs[f"{k}_total"] = np.asarray(p.get_total(t)) * np.ones_like(t)
+        arrs[f"{k}_polar"] = np.array([p.polar_x, p.polar_y])
+    train = P.PulseTrain(10.0, 3, P.ChirpedPulse(tau_0=3, e_start=-2.0, e0=1.0, t0=12), t_shift=1.0)
+    arrs["train_total"] = train.get_total(t)
+    fx, fy = train.get_total_xy(t)
+    arrs["train_x"], arrs["train_y"] = fx, fy
+    # integrals used by the non-uniform grid builders
+    arrs["chirped_integral"] = plist["chirped"].get_integral(t)
+    np.savez_compressed(os.path.join(HERE, "pyref_pulses.npz"), **arrs)
+
+    # tools: time grids, dm composition, concurrence, dynamical-map time-localisation
+    rng = np.random.default_rng(77)
+    p1 = P.ChirpedPulse(tau_0=3, e_start=0, e0=1, t0=20)
+    p2 = P.ChirpedPulse(tau_0=2, e_start=0, e0=1, t0=60)
+    ct = T.construct_t(0, 100, 0.1, 1.0, None, p1, p2)
+    ct_exp = T.construct_t(0, 400, 0.1, 2.0, 0.05, p1, simple_exp=True)
+    sg = T.simple_t_gaussian(0, 40, 200, 0.1, 1.0, p1)
+    outs = [np.arange(5.0)] + [rng.normal(size=5) + 1j * rng.normal(size=5) for _ in range(10)]
+    tdm, rdm = T.compose_dm(outs, dim=4)
+    rho4 = np.stack([rand_rho(4, rng) for _ in range(3)])
+    conc = np.array([T.concurrence(r) for r in rho4])
+    maps = rand_lindblad_maps(12, 2, 0.1, rng)
+    dm_cum = np.empty_like(maps)
+    acc = np.eye(4, dtype=complex)
+    for i in range(12):
+        acc = maps[i] @ acc
+        dm_cum[i] = acc
+    times = np.round(np.arange(13) * 0.1, 6)
+    tl = T.calc_tl_dynmap_pseudo(dm_cum, times)
+    ops_dm = {f"ops_dm_{k}": np.array(T.output_ops_dm(v)) for k, v in
+              {"2": 2, "6": 6, "21": [2, 1], "22": [2, 2], "222": [2, 2, 2]}.items()}
+    np.savez_compressed(os.path.join(HERE, "pyref_tools.npz"), construct_t=ct, construct_t_exp=ct_exp,
+                        simple_t_gaussian=sg, compose_in=np.array(outs, dtype=complex), compose_t=tdm,
+                        compose_rho=rdm, conc_rho=rho4, concurrence=conc, dm_cum=dm_cum, tl_times=times,
+                        tl_maps=tl, **ops_dm)
+
+
+if __name__ == "__main__":
+    if not fref.available():
+        raise SystemExit("build oracle/_ref first: make -C oracle ref")
+    gen_fortran()
+    gen_pyref()
+    tot = sum(os.path.getsize(os.path.join(HERE, f)) for f in os.listdir(HERE) if f.endswith(".npz"))
+    print(f"golden fixtures written: {tot/1e6:.2f} MB")

@@ -1,0 +1,296 @@
+"""HIP path (libpqd via the C-ABI) vs the CPU oracle and the reference's golden vectors. GPU only.
+
+Tolerances: the FP64 kernels and the oracle do the same arithmetic in different summation orders;
+relative differences stay at a few 1e-14 per step. Tests use 1e-11 (PT sweeps, with up to 1e2-step
+error growth) and 1e-12 elsewhere — far below the north-star bar (1e-8 abs no-phonon, 1e-6 rel with
+phonons)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+from pyaceqd_amd import engine, pt as ptmod
+from pyaceqd_amd.engine import MTO, Grid, System, Trajectories
+from tests import helpers as H
+
+pytestmark = pytest.mark.gpu
+F = lambda maps: np.asfortranarray(np.asarray(maps).transpose(1, 2, 0))  # noqa: E731
+
+
+def rel(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return float(np.max(np.abs(a - b)) / max(1e-300, np.max(np.abs(b))))
+
+
+def cmp_lists(got, ref, tol):
+    assert len(got) == len(ref)
+    for a, b in zip(got, ref):
+        assert a.shape == b.shape
+        assert rel(a, b) < tol, rel(a, b)
+
+
+# --------------------------------------------------------------------------------- free propagators
+@pytest.mark.parametrize("N,n_sub", [(2, 1), (3, 1), (4, 1), (4, 3), (5, 1), (6, 1), (6, 2)])
+def test_free_propagators(N, n_sub):
+    sysd, grid = H.random_system(N, n_steps=25, n_sub=n_sub, seed=N + 10 * n_sub)
+    got = engine.free_propagators(sysd, grid)
+    ref = oracle.free_propagators(sysd, grid)
+    assert rel(got, ref) < 1e-12
+
+
+# --------------------------------------------------------------------------------- sweeps
+def _traj(n_steps, N, n_traj, seed):
+    rng = np.random.default_rng(seed)
+    b = rng.integers(0, n_steps // 2, size=n_traj)
+    e = np.minimum(n_steps, b + rng.integers(1, n_steps, size=n_traj))
+    mt = []
+    for t in range(n_traj):
+        s = int(rng.integers(0, e[t] + 1))
+        A = rng.normal(size=(N, N)) + 1j * rng.normal(size=(N, N))
+        mt.append(MTO(t, s, bool(rng.integers(0, 2)), int(rng.integers(0, 3)), A / np.linalg.norm(A)))
+        if t % 2:
+            mt.append(MTO(t, s, False, 1, np.eye(N) * 0.5 + A / np.linalg.norm(A)))
+    return Trajectories(b, e, mt)
+
+
+@pytest.mark.parametrize("N", [2, 3, 4, 5, 6])
+@pytest.mark.parametrize("n_traj", [1, 3, 9])
+def test_sweep_no_pt(N, n_traj):
+    sysd, grid = H.random_system(N, n_steps=30, seed=N)
+    tr = _traj(grid.n_steps, N, n_traj, seed=N + n_traj)
+    ops = [H.ketbra(N, 0, 0), H.ketbra(N, N - 1, 0), np.eye(N)]
+    rho0 = H.random_rho(N)
+    cmp_lists(engine.propagate(sysd, grid, rho0, ops, tr), oracle.propagate(sysd, grid, rho0, ops, tr), 1e-12)
+
+
+@pytest.mark.parametrize("N", [2, 3, 4, 5, 6])
+@pytest.mark.parametrize("chi", [8, 16, 32, 64])
+def test_sweep_pt(N, chi):
+    sysd, grid = H.random_system(N, n_steps=24, seed=3 * N + chi)
+    pt = ptmod.random_pt(N, chi, D=min(N * N, 9), n_slices=7, seed=chi, eps=0.15)
+    tr = _traj(grid.n_steps, N, 6, seed=N * chi)
+    ops = [H.ketbra(N, 0, 0), H.ketbra(N, 1, 0), np.eye(N)]
+    rho0 = H.random_rho(N)
+    cmp_lists(engine.propagate(sysd, grid, rho0, ops, tr, pt=pt),
+              oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt), 1e-11)
+
+
+def test_sweep_pt_many_trajectories_and_ragged_windows():
+    N, chi = 4, 64
+    sysd, grid = H.random_system(N, n_steps=40, seed=99)
+    pt = ptmod.random_pt(N, chi, D=16, n_slices=41, seed=5, eps=0.1)
+    tr = _traj(grid.n_steps, N, 37, seed=1)
+    ops = [H.ketbra(N, a, b) for a in range(N) for b in range(N)]
+    rho0 = H.random_rho(N)
+    cmp_lists(engine.propagate(sysd, grid, rho0, ops, tr, pt=pt),
+              oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
+
+
+def test_empty_batch_and_zero_steps():
+    sysd, grid = H.random_system(2, n_steps=0, seed=0)
+    tr = Trajectories(np.array([0]), np.array([0]))
+    out = engine.propagate(sysd, grid, H.ketbra(2, 0, 0), [np.eye(2)], tr)
+    assert out[0].shape == (1, 1) and abs(out[0][0, 0] - 1) < 1e-15
+    out = engine.propagate(sysd, Grid(0, 0.1, 5), H.ketbra(2, 0, 0), [np.eye(2)], Trajectories(np.array([]), np.array([])))
+    assert out == []
+
+
+def test_invalid_arguments_raise():
+    sysd, grid = H.random_system(2, n_steps=5, seed=0)
+    with pytest.raises(ValueError, match="window"):
+        engine.propagate(sysd, grid, H.ketbra(2, 0, 0), [np.eye(2)], Trajectories(np.array([0]), np.array([6])))
+    with pytest.raises(ValueError, match="MTO"):
+        engine.propagate(sysd, grid, H.ketbra(2, 0, 0), [np.eye(2)],
+                         Trajectories(np.array([0]), np.array([5]), [MTO(0, 9, False, 1, np.eye(2))]))
+
+
+# --------------------------------------------------------------------------------- full-size properties (C3)
+def test_c3_full_size_invariants():
+    """biexciton N=4, chi=64, 10,000 steps: structured PT == bare dynamics; trace preserved"""
+    from pyaceqd_amd.four_level_system.linear import biexciton_ops
+    from pyaceqd_amd import opgrammar
+    from pyaceqd_amd.constants import hbar
+    N, dt, n = 4, 0.1, 10000
+    so, bo, lo, io, _ = biexciton_ops(delta_b=4, lindblad=True)
+    from pyaceqd_amd.pulses import ChirpedPulse, PulseTrain
+    train = PulseTrain(100, 10, ChirpedPulse(tau_0=3, e_start=-2.0, e0=1.0, t0=12))
+    ds = dt / 4
+    ts = ds * np.arange(4 * n + 1)
+    fx = train.get_total(ts)
+    sysd = System(dim=N, H0=sum(opgrammar.to_matrix(s, N) for s in so),
+                  lindblad=[(r, opgrammar.to_matrix(o, N)) for o, r in lo],
+                  channels=[(-0.5 * np.pi * hbar * opgrammar.to_matrix(io[0][0], N), fx)], sample_dt=ds)
+    grid = Grid(0.0, dt, n)
+    pt = ptmod.synthetic_pt(opgrammar.to_matrix(bo, N), chi=64, n_init=410, n_rep=1)
+    ops = [opgrammar.to_matrix(f"|{k}><{k}|_4", N) for k in range(4)] + [np.eye(N)]
+    tr = Trajectories(np.zeros(8, dtype=int), np.full(8, n))
+    rho0 = H.ketbra(N, 0, 0)
+    a = engine.propagate(sysd, grid, rho0, ops, tr, pt=pt)
+    b = engine.propagate(sysd, grid, rho0, ops, tr)
+    for x, y in zip(a, b):
+        assert np.max(np.abs(x - y)) < 1e-10
+        assert np.max(np.abs(x[:, -1] - 1)) < 1e-10
+    # the pulse train actually drives the system
+    assert np.max(np.abs(b[0][:, 3])) > 1e-3
+
+
+# --------------------------------------------------------------------------------- plan API
+def test_plan_repeat_is_deterministic():
+    N = 4
+    sysd, grid = H.random_system(N, n_steps=50, seed=4)
+    pt = ptmod.random_pt(N, 32, D=9, n_slices=4, seed=1, eps=0.1)
+    tr = _traj(grid.n_steps, N, 10, seed=2)
+    ops = [H.ketbra(N, 1, 1)]
+    plan = engine.Plan(sysd, grid, H.random_rho(N), ops, tr, pt=pt)
+    plan.execute()
+    a = plan.download()
+    plan.execute(rebuild_free=False)
+    plan.execute()
+    b = plan.download()
+    f, w, k = plan.timing()
+    assert k == 3 and w > 0 and f >= 0
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+
+
+# --------------------------------------------------------------------------------- map-chain sweeps vs Fortran
+def load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name))
+
+
+@pytest.mark.parametrize("dim", [2, 4, 6])
+def test_mapchain_vs_fortran_golden(golden_dir, dim):
+    from pyaceqd_amd.two_time import propagate_tau_module as M
+    z = load(golden_dir, f"fortran_propagate_tau_d{dim}.npz")
+    assert rel(M.propagate_tau(F(z["dm_tl"]), z["rho_init"], int(z["n_tau"]), dim, int(z["j_start"])), z["rho_out"]) < 1e-12
+    z = load(golden_dir, f"fortran_onetime_d{dim}.npz")
+    r = M.calc_onetime_parallel(F(z["dm_tl"]), z["rho_init"], int(z["n_tau"]), dim, z["opa"], z["opb"], z["opc"],
+                                z["time"], z["time_sparse"])
+    assert rel(r, z["result"]) < 1e-12
+    z = load(golden_dir, f"fortran_onetime_block_d{dim}.npz")
+    r = M.calc_onetime_parallel_block(dm_block=F(z["dm_block"]), dm_s=z["dm_s"], rho_init=z["rho_init"],
+                                      n_tb=int(z["n_tb"]), nx_tau=int(z["nx_tau"]), dim=dim, opa=z["opa"],
+                                      opb=z["opb"], opc=z["opc"], time=z["time"], time_sparse=z["time_sparse"])
+    assert rel(r, z["result"]) < 1e-12
+    z = load(golden_dir, f"fortran_twotime_phonon_block_d{dim}.npz")
+    r = M.calc_twotime_phonon_block(dm_taucs2=np.asfortranarray(z["dm_taucs2"].transpose(2, 3, 0, 1)),
+                                    dm_sep1=F(z["dm_sep1"]), dm_sep2=F(z["dm_sep2"]), dm_s=z["dm_s"],
+                                    rho_init=z["rho_init"], n_tb=int(z["n_tb"]), nx_tau=int(z["nx_tau"]), dim=dim,
+                                    opa=z["opa"], opb=z["opb"], opc=z["opc"], time=z["time"],
+                                    time_sparse=z["time_sparse"])
+    assert rel(r, z["result"]) < 1e-12
+
+
+@pytest.mark.parametrize("dim", [2, 4, 5])
+def test_timebin_vs_fortran_golden(golden_dir, dim):
+    from pyaceqd_amd.timebin import timebin_tl as TB
+    z = load(golden_dir, f"fortran_timebin_d{dim}.npz")
+    a = (F(z["dm_1"]), F(z["dm_2"]), z["rho_init"], z["t1"], F(z["precalc"]), float(z["dt"]), dim)
+    o = list(z["ops8"])
+    tb = float(z["tb"])
+    assert rel(TB.four_time_8op(*a, *o, False, False, tb), z["result8"]) < 1e-12
+    assert rel(TB.four_time_8op(*a, *o, True, False, tb), z["result8_early"]) < 1e-12
+    assert rel(TB.four_time_8op(*a, *o, False, True, tb), z["result8_late"]) < 1e-12
+    assert rel(TB.four_time(*a, *o[:4], tb), z["result4"]) < 1e-12
+    assert rel(TB.dynamics_t1(*a, tb), z["dyn_t1"]) < 1e-12
+
+
+def test_mapchain_large_vs_oracle():
+    """C4-shaped map-chain sweep (256 t1 points x 2000 tau steps, N=4) vs the C oracle"""
+    from pyaceqd_amd.two_time import propagate_tau_module as M
+    rng = np.random.default_rng(0)
+    dim, n_tau = 4, 2000
+    N2 = dim * dim
+    n_tfull = 256 + n_tau + 2
+    base = np.eye(N2) + 0.02 * (rng.normal(size=(N2, N2)) + 1j * rng.normal(size=(N2, N2)))
+    base /= np.max(np.abs(np.linalg.eigvals(base)))
+    maps = np.stack([base] * (n_tfull - 1)) * (1 + 1e-4 * rng.normal(size=(n_tfull - 1, 1, 1)))
+    time = np.round(np.arange(n_tfull) * 0.1, 6)
+    ts = np.round(np.arange(256) * 0.1, 6)
+    ops = [rng.normal(size=(dim, dim)) + 1j * rng.normal(size=(dim, dim)) for _ in range(3)]
+    rho = H.random_rho(dim).reshape(N2)
+    a = M.calc_onetime_parallel(F(maps), rho, n_tau, dim, *ops, time, ts)
+    b = oracle.calc_onetime_parallel(F(maps), rho, n_tau, dim, *ops, time, ts, nthreads=8)
+    assert rel(a, b) < 1e-11
+
+
+# --------------------------------------------------------------------------------- drop-in driver
+def _oracle_patch(monkeypatch):
+    """route general_system's propagate through the oracle (same lowering, CPU arithmetic)"""
+    from pyaceqd_amd.general_system import general_system as gs
+
+    def prop(system, grid, rho0, out_ops, traj, pt=None, ctx=None):
+        return oracle.propagate(system, grid, rho0, out_ops, traj, pt=pt, nthreads=8)
+    monkeypatch.setattr(gs, "propagate", prop)
+
+
+def test_tls_rabi_kat():
+    from pyaceqd_amd.two_level_system.tls import tls
+    from pyaceqd_amd.pulses import ChirpedPulse
+    for e0 in (0.5, 1.0, 2.0):
+        t, g, x, p, _ = tls(0, 40, ChirpedPulse(tau_0=3, e_start=0, e0=e0, t0=20), dt=0.05)
+        assert abs(x[-1].real - np.sin(np.pi * e0 / 2) ** 2) < 1e-6
+        assert np.max(np.abs(g + x - 1)) < 1e-12
+
+
+def test_tls_c1_vs_oracle(monkeypatch):
+    """config C1: tls(0,100, ChirpedPulse(tau_0=3, e_start=0, e0=1, t0=20), dt=0.1, lindblad=True)"""
+    from pyaceqd_amd.two_level_system.tls import tls
+    from pyaceqd_amd.pulses import ChirpedPulse
+    args = dict(dt=0.1, lindblad=True)
+    p = ChirpedPulse(tau_0=3, e_start=0, e0=1, t0=20)
+    a = tls(0, 100, p, **args)
+    assert a.shape == (5, 1001)
+    _oracle_patch(monkeypatch)
+    b = tls(0, 100, p, **args)
+    assert np.max(np.abs(a - b)) < 1e-12
+
+
+def test_biexciton_and_sixls_vs_oracle(monkeypatch, tmp_path):
+    from pyaceqd_amd.four_level_system.linear import biexciton
+    from pyaceqd_amd.six_level_system.linear import sixls_linear
+    from pyaceqd_amd.pulses import ChirpedPulse
+    from pyaceqd_amd import opgrammar
+    pfile = str(tmp_path / "bx.npz")
+    ptmod.save_pt(pfile, ptmod.random_pt(4, 32, D=9, n_slices=30, seed=3, eps=0.05), dim=4)
+    p = ChirpedPulse(tau_0=3, e_start=-2.0, e0=1.0, t0=12, polar_x=0.8)
+    runs = [lambda: biexciton(0, 30, p, dt=0.1, delta_xy=0.02, lindblad=True, phonons=True, pt_file=pfile),
+            lambda: sixls_linear(0, 30, p, dt=0.1, bx=2.0, bz=0.5, lindblad=True, output_dm=True)]
+    got = [r() for r in runs]
+    _oracle_patch(monkeypatch)
+    ref = [r() for r in runs]
+    assert rel(got[0], ref[0]) < 1e-11
+    assert rel(got[1][1], ref[1][1]) < 1e-12
+
+
+def test_three_op_two_time_vs_oracle(monkeypatch, tmp_path):
+    """C4-shaped two-time G2 sweep through the batched driver (small sizes)"""
+    from pyaceqd_amd.four_level_system.linear import biexciton
+    from pyaceqd_amd.two_time.correlations import three_op_two_time
+    from pyaceqd_amd.pulses import ChirpedPulse
+    pfile = str(tmp_path / "bx.npz")
+    ptmod.save_pt(pfile, ptmod.synthetic_pt(np.diag([0, 1, 1, 2.0]), chi=16, n_init=20, n_rep=2, structured=False,
+                                             eps=0.05), dim=4)
+    p = ChirpedPulse(tau_0=3, e_start=-2.0, e0=1.0, t0=5)
+    t_axis = np.round(np.arange(12) * 0.5, 6)
+    kw = dict(opA="|3><1|_4", opB="|1><1|_4", opC="|1><3|_4", tau_max=8.0, dt=0.1)
+    opts = lambda: {"lindblad": True, "phonons": True, "pt_file": pfile}  # noqa: E731
+    t1, tau, G = three_op_two_time(biexciton, t_axis, p, options=opts(), **kw)
+    assert G.shape == (12, 81)
+    _oracle_patch(monkeypatch)
+    _, _, Gr = three_op_two_time(biexciton, t_axis, p, options=opts(), **kw)
+    assert rel(G, Gr) < 1e-10
+
+
+def test_calc_dynmap_consistency():
+    from pyaceqd_amd.two_level_system.tls import tls
+    from pyaceqd_amd.pulses import ChirpedPulse
+    p = ChirpedPulse(tau_0=2, e_start=0.1, e0=1.3, t0=5)
+    rho0 = np.array([[0.7, 0.2], [0.2, 0.3]], dtype=complex)
+    res, dm = tls(0, 10, p, dt=0.1, lindblad=True, calc_dynmap=True, rho0=rho0)
+    direct = tls(0, 10, p, dt=0.1, lindblad=True, rho0=rho0)
+    assert dm.shape == (100, 4, 4)
+    assert np.max(np.abs(res - direct)) < 1e-12
+    rho_end = (dm[-1] @ rho0.reshape(4)).reshape(2, 2)
+    assert abs(rho_end[1, 1] - direct[2][-1]) < 1e-12
