@@ -78,13 +78,15 @@ def cpu_baseline(chi, target_s=15.0):
     from oracle import oracle
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
     threads = max(1, min(threads, 16))
-    # calibrate on 1 trajectory x 60 steps
-    sysd, grid, pt, rho0, ops, tr = build_workload(1, 60, chi)
-    t0 = time.perf_counter()
-    oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt, nthreads=1)
-    per = (time.perf_counter() - t0) / 61
+    # calibrate on the same shape with all threads (setup + free propagators included, as in the sample)
     n_traj = 2 * threads
-    steps = int(max(50, min(10000, target_s * threads / per / n_traj)))
+    sysd, grid, pt, rho0, ops, tr = build_workload(n_traj, 300, chi)
+    t0 = time.perf_counter()
+    oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt, nthreads=threads)
+    per = (time.perf_counter() - t0) / float(np.sum(tr.out_end + 1))  # seconds per traj-step
+    total = target_s / per                                   # traj-steps that fill ~target_s
+    steps = int(max(50, min(10000, total / n_traj)))
+    n_traj = int(min(4096, max(n_traj, threads * round(total / steps / threads))))
     sysd, grid, pt, rho0, ops, tr = build_workload(n_traj, steps, chi)
     t0 = time.perf_counter()
     oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt, nthreads=threads)

@@ -63,6 +63,7 @@ struct SweepParams {
     const int4* ev;          // (step, after?1:0, superop index, 0), sorted per trajectory
     const double2* sop;      // MTO superoperators N2*N2 each
     double2* out;
+    int ablate;              // diagnostics only (PQD_ABLATE): 1 skip PT, 2 skip column phases, 4 skip outputs
 };
 
 // map-chain (Fortran f2py equivalents)

@@ -11,6 +11,7 @@
 #include <complex>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -457,6 +458,7 @@ int pqd_plan_create(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* grid, c
     }
     sp.sched = P->sched.p; sp.rho0 = P->rho0.p; sp.n_out = n_out; sp.ovec = P->ovec.p;
     sp.blk_traj = P->blk_traj.p; sp.blk_end = P->blk_end.p; sp.wbeg = P->wbeg.p; sp.wend = P->wend.p;
+    { const char* ab = getenv("PQD_ABLATE"); sp.ablate = ab ? atoi(ab) : 0; }
     sp.woff = P->woff.p; sp.ev_start = P->ev_start.p; sp.ev = P->ev.p; sp.sop = P->sop.p; sp.out = P->out.p;
     HIPCHK(hipStreamSynchronize(s));
     *out = guard.release();

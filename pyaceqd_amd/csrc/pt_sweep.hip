@@ -53,7 +53,8 @@ __device__ __forceinline__ void col_apply(const double2* __restrict__ Op, double
 }
 
 template <int N2, int CHI>
-__global__ __launch_bounds__(256) void pt_sweep_kernel(SweepParams p) {
+__global__ __launch_bounds__(256) void pt_sweep_kernel(SweepParams p, const double2* __restrict__ Mg,
+                                                       const double2* __restrict__ Qg0, double2* __restrict__ outg) {
     using L = SweepLayout<N2, CHI>;
     constexpr int RS = L::RS, TS = L::TS, KD = L::KD, NCOL = L::NCOL;
     extern __shared__ __attribute__((aligned(16))) double2 smem[];
@@ -102,7 +103,7 @@ __global__ __launch_bounds__(256) void pt_sweep_kernel(SweepParams p) {
         bool need = false;
 #pragma unroll
         for (int b = 0; b < BT; ++b) need |= (s_wb[b] <= n) & (n <= s_we[b]);
-        if (need) {
+        if (need && !(p.ablate & 4)) {
             const double2* cvec = (n == 0) ? p.closure0 : p.closure + (size_t)p.sched[n - 1] * CHI;
             constexpr int NPART = BT * N2 * 4;
             for (int it = 0; it < (NPART + 255) / 256; ++it) {
@@ -126,15 +127,15 @@ __global__ __launch_bounds__(256) void pt_sweep_kernel(SweepParams p) {
                     double2 s = c_zero();
                     const double2* ov = p.ovec + (size_t)k * N2;
                     for (int a = 0; a < N2; ++a) c_fma(s, ov[a], rbuf[b * N2 + a]);
-                    p.out[s_wo[b] + (long long)(n - s_wb[b]) * p.n_out + k] = s;
+                    outg[s_wo[b] + (long long)(n - s_wb[b]) * p.n_out + k] = s;
                 }
             }
         }
         if (n >= n_end) break;
 
         // ------------------------------------------------------------ column phase A
-        const double2* Ma = p.M + (size_t)(2 * n) * N2 * N2;
-        if (colthr) {
+        const double2* Ma = Mg + (size_t)(2 * n) * N2 * N2;
+        if (colthr && !(p.ablate & 2)) {
             while (ev_cur < ev_lim) {  // applyBefore-false MTOs at step n
                 const int4 e = p.ev[ev_cur];
                 if (e.x != n || e.y != 1) break;
@@ -146,8 +147,8 @@ __global__ __launch_bounds__(256) void pt_sweep_kernel(SweepParams p) {
         __syncthreads();
 
         // ------------------------------------------------------------ PT contraction
-        {
-            const double2* Qs = p.Q + (size_t)p.sched[n] * p.D * CHI * CHI;
+        if (!(p.ablate & 1)) {
+            const double2* Qs = Qg0 + (size_t)p.sched[n] * p.D * CHI * CHI;
             for (int a = wave; a < N2; a += 4) {
                 const double2* Qg = Qs + (size_t)p.gmap[a] * CHI * CHI + pj;
                 const double2* xr = st + a * RS + pq;
@@ -217,7 +218,7 @@ __global__ __launch_bounds__(256) void pt_sweep_kernel(SweepParams p) {
 
         // ------------------------------------------------------------ column phase B
         const double2* Mb = Ma + N2 * N2;
-        if (colthr) {
+        if (colthr && !(p.ablate & 2)) {
             col_apply<N2, RS>(Mb, col);
             while (ev_cur < ev_lim) {  // applyBefore-true MTOs at step n+1
                 const int4 e = p.ev[ev_cur];
@@ -304,7 +305,7 @@ hipError_t launch_sw(int n_blocks, const SweepParams& p, hipStream_t s) {
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((pt_sweep_kernel<N2, CHI>), dim3(n_blocks), dim3(256), L::LDS, s, p);
+    hipLaunchKernelGGL((pt_sweep_kernel<N2, CHI>), dim3(n_blocks), dim3(256), L::LDS, s, p, p.M, p.Q, p.out);
     return hipGetLastError();
 }
 

@@ -1,0 +1,53 @@
+"""Sharding of independent propagation units over ranks (one process per GPU).
+
+The reference's only parallelism is a host thread pool of independent ACE processes (one per t1
+point or parameter point: correlations.py:153-169, rabi_rotations.py:172-198,
+pol_entanglement/G2.py:486-497) — embarrassingly parallel, results gathered in Python lists.
+Here the units (t1 points of a two-time sweep, or points of a pulse/B-field scan) are split into
+contiguous blocks, one per rank; each rank runs its block as one batched launch on its own GPU and
+there is no per-step communication. The only exchange is an optional gather of the finished blocks
+to rank 0 (torch.distributed: RCCL over xGMI on the GPU box, gloo on CPU).
+"""
+import numpy as np
+
+
+def shard_range(n_units, rank, world):
+    """contiguous block [lo, hi) of rank `rank` (sizes differ by at most one)"""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError(f"bad rank/world {rank}/{world}")
+    base, extra = divmod(int(n_units), int(world))
+    lo = rank * base + min(rank, extra)
+    hi = lo + base + (1 if rank < extra else 0)
+    return lo, hi
+
+
+def shard(units, rank, world):
+    lo, hi = shard_range(len(units), rank, world)
+    return units[lo:hi]
+
+
+def gather_blocks(local, dist=None, dst=0):
+    """Gather each rank's list of per-unit results (numpy arrays) to `dst` in rank order.
+    Returns the concatenated list on dst, None elsewhere (or `local` when not distributed)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return list(local)
+    world = dist.get_world_size()
+    objs = [None] * world if dist.get_rank() == dst else None
+    dist.gather_object([np.asarray(x) for x in local], objs, dst=dst)
+    if dist.get_rank() != dst:
+        return None
+    out = []
+    for blk in objs:
+        out.extend(blk)
+    return out
+
+
+def run_sharded(units, work, dist=None):
+    """Run `work(block_of_units) -> list of results` on this rank's block and gather to rank 0."""
+    if dist is not None and dist.is_initialized():
+        rank, world = dist.get_rank(), dist.get_world_size()
+    else:
+        rank, world = 0, 1
+    mine = shard(list(units), rank, world)
+    res = work(mine) if len(mine) else []
+    return gather_blocks(res, dist)
