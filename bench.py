@@ -1,18 +1,19 @@
 """bench.py — propagation steps/s of the 4-level biexciton PT propagator at bond dimension 64.
 
-Workload (BASELINE.json metric): every rank runs the two-time G2(t1, tau)
-sweep of the biexciton cascade (N=4, delta_b=4, lindblad, dt=0.1 ps, pulse train
-PulseTrain(100, 10, ChirpedPulse(tau_0=3, e_start=-2, e0, t0=12))), with a chi=64 synthetic PT
-(I + 0.05 G/sqrt(chi) per slice, spectral radius <= 1, 410 initial slices + 1 repeated
-slice, no dictionary compression: D = N^2 = 16). n_traj t1 points (t1 = 0, 0.1, ... ps), each a
-trajectory with the MTOs A=|3><1| (right) and C=|1><3| (left) at t1 and outputs <B>=<|1><1|> and
-<ABC> over tau = 0..1000 ps (n_tau = 10,000). Ranks form a pulse-area scan (e0 = 1 + 0.1 rank), so the
-per-GPU work is fixed (weak scaling) and there is no data-path collective.
+Workload (BASELINE.json metric; SURVEY.md §8d C3 system, C4 sweep shape, C5 scan structure): each GPU
+runs a pulse-area scan of two-time G2(t1, tau) sweeps of the biexciton cascade (N=4, delta_b=4,
+lindblad, dt=0.1 ps, pulse train PulseTrain(100, 10, ChirpedPulse(tau_0=3, e_start=-2, e0, t0=12))):
+`--scan` pulse areas e0 per GPU (rank r takes scan points [r*scan, (r+1)*scan), e0 = 1 + 0.05 k), each
+with the C4 t1 grid of `--t1` points (t1 = 0, 0.1, ... ps). Every (e0, t1) pair is one trajectory
+with the MTOs A=|3><1| (right) and C=|1><3| (left) at t1, outputs <B>=<|1><1|> and <ABC> for
+tau = 0..1000 ps (n_tau = 10,000). The bath is a chi=64 synthetic PT (I + 0.05 G/sqrt(chi)
+per slice, spectral radius <= 1; 410 initial slices + 1 repeated slice; D = N^2 = 16, no dictionary).
+Per-GPU work is fixed (weak scaling); there is no data-path collective.
 
-One bench step = one execution of the device-resident plan: free-propagator build for all 2*n_steps
-half steps + the lock-step PT sweep of all trajectories. Inputs (PT, operators, pulse samples) are
+One bench step = one execution of the device-resident plan: free-propagator build for all systems and
+half steps + the lock-step PT sweep of every trajectory. Inputs (PT, operators, pulse samples) are
 resident in HBM before the timed region. value = whole-job useful trajectory-steps per second
-(n_traj * n_tau per rank; the redundant trunk re-propagation 0 -> t1 is executed but not counted).
+(n_traj * n_tau per GPU; the trunk re-propagation 0 -> t1 (<= 25.5 ps) is executed but not counted).
 """
 import argparse
 import json
@@ -29,35 +30,44 @@ PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 (vector == matrix on gfx950), spec
 PEAK_HBM_GBS = 8000.0
 
 
-def build_workload(n_traj, n_tau, chi, rank=0, dt=0.1, seed=1234):
+def build_workload(n_t1, n_tau, chi, scan=1, scan_offset=0, dt=0.1, seed=1234):
+    """(systems, grid, pt, rho0, ops, traj): `scan` pulse-area points x `n_t1` t1 points"""
     from pyaceqd_amd import engine, opgrammar, pt as ptmod
     from pyaceqd_amd.constants import hbar
     from pyaceqd_amd.four_level_system.linear import biexciton_ops
     from pyaceqd_amd.pulses import ChirpedPulse, PulseTrain
     N = 4
     so, bo, lo, io, _ = biexciton_ops(delta_b=4, lindblad=True)
-    t1_steps = np.arange(n_traj)
+    t1_steps = np.arange(n_t1)
     n_steps = int(t1_steps[-1] + n_tau)
     ds = dt / 4
     ts = ds * np.arange(4 * n_steps + 1)
-    e0 = 1.0 + 0.1 * rank
-    train = PulseTrain(100, 10, ChirpedPulse(tau_0=3, e_start=-2.0, e0=e0, t0=12, polar_x=1.0))
-    fx, fy = train.get_total_xy(ts)
     mat = lambda s: opgrammar.to_matrix(s, N)  # noqa: E731
-    chans = [(-0.5 * np.pi * hbar * mat(op), fx if pol == "x" else fy) for op, pol in io]
-    sysd = engine.System(dim=N, H0=sum(mat(s) for s in so), lindblad=[(r, mat(o)) for o, r in lo],
-                         channels=chans, sample_t0=0.0, sample_dt=ds)
+    H0 = sum(mat(s) for s in so)
+    lind = [(r, mat(o)) for o, r in lo]
+    systems = []
+    for k in range(scan):
+        e0 = 1.0 + 0.05 * (scan_offset + k)
+        train = PulseTrain(100, 10, ChirpedPulse(tau_0=3, e_start=-2.0, e0=e0, t0=12, polar_x=1.0))
+        fx, fy = train.get_total_xy(ts)
+        chans = [(-0.5 * np.pi * hbar * mat(op), fx if pol == "x" else fy) for op, pol in io]
+        systems.append(engine.System(dim=N, H0=H0, lindblad=lind, channels=chans, sample_t0=0.0, sample_dt=ds))
     grid = engine.Grid(0.0, dt, n_steps, 1)
     pt = ptmod.synthetic_pt(mat(bo), chi=chi, n_init=min(410, n_steps), n_rep=1, seed=seed, eps=0.05, dt=dt)
     A, B, Cm = mat("|3><1|_4"), mat("|1><1|_4"), mat("|1><3|_4")
-    mtos = []
-    for t in range(n_traj):
-        mtos.append(engine.MTO(t, int(t1_steps[t]), False, 2, A))
-        mtos.append(engine.MTO(t, int(t1_steps[t]), False, 1, Cm))
-    tr = engine.Trajectories(t1_steps.copy(), t1_steps + n_tau, mtos)
+    mtos, beg, end, sysidx = [], [], [], []
+    for k in range(scan):
+        for t1 in t1_steps:
+            t = len(beg)
+            mtos.append(engine.MTO(t, int(t1), False, 2, A))
+            mtos.append(engine.MTO(t, int(t1), False, 1, Cm))
+            beg.append(int(t1))
+            end.append(int(t1) + n_tau)
+            sysidx.append(k)
+    tr = engine.Trajectories(np.array(beg), np.array(end), mtos, system=np.array(sysidx))
     ops = [B, A @ B @ Cm]
     rho0 = mat("|0><0|_4")
-    return sysd, grid, pt, rho0, ops, tr
+    return (systems if scan > 1 else systems[0]), grid, pt, rho0, ops, tr
 
 
 def flops_per_traj_step(N=4, chi=64, n_out=2):
@@ -102,7 +112,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--traj", type=int, default=1024, help="t1 trajectories per GPU")
+    ap.add_argument("--t1", type=int, default=256, help="t1 points per scan point (C4 grid)")
+    ap.add_argument("--scan", type=int, default=8, help="pulse-area scan points per GPU")
     ap.add_argument("--n-tau", type=int, default=10000)
     ap.add_argument("--chi", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -124,7 +135,9 @@ def main():
 
     from pyaceqd_amd import _lib, engine
     ctx = _lib.context(local)
-    sysd, grid, pt, rho0, ops, tr = build_workload(args.traj, args.n_tau, args.chi, rank=rank)
+    sysd, grid, pt, rho0, ops, tr = build_workload(args.t1, args.n_tau, args.chi, scan=args.scan,
+                                                   scan_offset=rank * args.scan)
+    n_traj = tr.n_traj
     plan = engine.Plan(sysd, grid, rho0, ops, tr, pt=pt, ctx=ctx)
 
     def barrier():
@@ -161,7 +174,7 @@ def main():
     g0 = np.array([r[0, 1] for r in res])
     assert np.all(np.isfinite(g0)), "non-finite output"
 
-    useful = args.traj * args.n_tau
+    useful = n_traj * args.n_tau
     executed = int(np.sum(tr.out_end + 1))
     value = useful * args.steps * world / el
     F = flops_per_traj_step(4, args.chi, len(ops))
@@ -181,14 +194,15 @@ def main():
         "data": "synthetic (SURVEY.md §8d: pulse train + synthetic chi=64 PT)",
         "config": {"workload": "biexciton two-time G2 sweep (C3 metric config, C4 shape, C5 scan over ranks)",
                    "N": 4, "chi": args.chi, "D": 16, "dt_ps": 0.1, "n_tau": args.n_tau,
-                   "traj_per_gpu": args.traj, "grid_steps": grid.n_steps,
+                   "traj_per_gpu": n_traj, "scan_points_per_gpu": args.scan, "t1_points": args.t1,
+                   "grid_steps": grid.n_steps,
                    "useful_traj_steps_per_gpu": useful, "executed_traj_steps_per_gpu": executed,
                    "parallelism": f"scan{world}", "kernel_ms": {"pt_sweep": ms_sweep, "free_prop": ms_free}},
         "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tf / PEAK_FP64_TFLOPS, "traffic": None,
                      "kernel": "pt_sweep_kernel<16,64>",
                      "algorithmic": f"{F} flop/traj-step x {executed} executed traj-steps per launch",
-                     "hbm_algorithmic_GBs": bytes_per_launch(grid.n_steps, 410, args.chi, n_traj=args.traj,
+                     "hbm_algorithmic_GBs": bytes_per_launch(grid.n_steps, 410, args.chi, n_traj=n_traj,
                                                              executed_steps=executed) / (ms_sweep * 1e-3) / 1e9},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -119,10 +119,22 @@ int pqd_propagate(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* grid, con
                   const int32_t* sched, const pqd_c128* rho0, int32_t n_out, const pqd_c128* out_ops,
                   const pqd_traj* traj, pqd_c128* out, int64_t out_len);
 
-/* device-resident plan for repeated execution (bench, scans): same arguments as pqd_propagate. */
+/* multi-system batch (pulse / field parameter scans): n_sys systems of equal dim share
+ * grid, PT, initial state and output operators; trajectory t uses systems[traj_sys[t]]. This replaces the
+ * caller-side scan loops over ACE runs (rabi_rotations.py:172-198, the C5 pulse/B-field scan). */
+int pqd_propagate_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems, const int32_t* traj_sys,
+                        const pqd_grid* grid, const pqd_pt* pt, const int32_t* sched, const pqd_c128* rho0,
+                        int32_t n_out, const pqd_c128* out_ops, const pqd_traj* traj, pqd_c128* out,
+                        int64_t out_len);
+
+/* device-resident plan for repeated execution (bench, scans): same arguments as pqd_propagate(_multi). */
 int pqd_plan_create(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* grid, const pqd_pt* pt,
                     const int32_t* sched, const pqd_c128* rho0, int32_t n_out, const pqd_c128* out_ops,
                     const pqd_traj* traj, int64_t out_len, pqd_plan** out);
+int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems, const int32_t* traj_sys,
+                          const pqd_grid* grid, const pqd_pt* pt, const int32_t* sched, const pqd_c128* rho0,
+                          int32_t n_out, const pqd_c128* out_ops, const pqd_traj* traj, int64_t out_len,
+                          pqd_plan** out);
 /* enqueue free-propagator build (if rebuild_free) + sweep on the context stream (asynchronous) */
 int pqd_plan_execute(pqd_plan* plan, int32_t rebuild_free);
 /* device pointer of the plan's output buffer (out_len complex values) */

@@ -111,8 +111,23 @@ def expm(A):
 
 
 def propagate(system, grid, rho0, out_ops, traj, pt=None, M=None, nthreads=1):
-    """Same contract as pyaceqd_amd.engine.propagate (list of (window, n_out) arrays)."""
-    from pyaceqd_amd.engine import split_output
+    """Same contract as pyaceqd_amd.engine.propagate (list of (window, n_out) arrays); a list of systems
+    with traj.system is handled by running each system's trajectories separately."""
+    from pyaceqd_amd.engine import split_output, Trajectories
+    if isinstance(system, (list, tuple)):
+        res = [None] * traj.n_traj
+        sysidx = np.asarray(traj.system if traj.system is not None else np.zeros(traj.n_traj, dtype=int))
+        for k, sy in enumerate(system):
+            ids = np.nonzero(sysidx == k)[0]
+            if len(ids) == 0:
+                continue
+            remap = {int(t): i for i, t in enumerate(ids)}
+            sub = Trajectories(np.asarray(traj.out_begin)[ids], np.asarray(traj.out_end)[ids],
+                               [type(m)(remap[m.traj], m.step, m.before, m.kind, m.op) for m in traj.mtos
+                                if m.traj in remap])
+            for i, r in zip(ids, propagate(sy, grid, rho0, out_ops, sub, pt=pt, nthreads=nthreads)):
+                res[i] = r
+        return res
     keep = []
     N = system.dim
     s = _system(system, keep)

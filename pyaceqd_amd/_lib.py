@@ -63,6 +63,11 @@ _SIGS = {
     "pqd_free_propagators": ([C.c_void_p, C.POINTER(pqd_system), C.POINTER(pqd_grid), P_C128], C.c_int),
     "pqd_propagate": ([C.c_void_p, C.POINTER(pqd_system), C.POINTER(pqd_grid), C.c_void_p, P_I32, P_C128,
                        C.c_int32, P_C128, C.POINTER(pqd_traj), P_C128, C.c_int64], C.c_int),
+    "pqd_propagate_multi": ([C.c_void_p, C.c_int32, C.POINTER(pqd_system), P_I32, C.POINTER(pqd_grid), C.c_void_p,
+                             P_I32, P_C128, C.c_int32, P_C128, C.POINTER(pqd_traj), P_C128, C.c_int64], C.c_int),
+    "pqd_plan_create_multi": ([C.c_void_p, C.c_int32, C.POINTER(pqd_system), P_I32, C.POINTER(pqd_grid),
+                               C.c_void_p, P_I32, P_C128, C.c_int32, P_C128, C.POINTER(pqd_traj), C.c_int64,
+                               C.POINTER(C.c_void_p)], C.c_int),
     "pqd_plan_create": ([C.c_void_p, C.POINTER(pqd_system), C.POINTER(pqd_grid), C.c_void_p, P_I32, P_C128,
                          C.c_int32, P_C128, C.POINTER(pqd_traj), C.c_int64, C.POINTER(C.c_void_p)], C.c_int),
     "pqd_plan_execute": ([C.c_void_p, C.c_int32], C.c_int),

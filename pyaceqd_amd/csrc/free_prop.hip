@@ -13,7 +13,7 @@
 
 namespace {
 
-__device__ __forceinline__ double2 sample_ch(const FreePropParams& p, int c, double t) {
+__device__ __forceinline__ double2 sample_ch(const FreePropSys& p, int c, double t) {
     const double2* f = p.samples + (size_t)c * p.n_samples;
     const int ns = p.n_samples;
     const double u = (t - p.s_t0) / p.s_dt;
@@ -47,8 +47,10 @@ __global__ __launch_bounds__(256) void free_prop_kernel(FreePropParams p) {
     __shared__ int s_sh;
 
     const int tid = threadIdx.x;
-    const int m = blockIdx.x;
+    const int si = blockIdx.x / (2 * p.n_steps);
+    const int m = blockIdx.x - si * 2 * p.n_steps;
     const int n = m >> 1, h = m & 1;
+    const FreePropSys sy = p.systems[si];
     const int nsub = p.n_sub > 0 ? p.n_sub : 1;
     const double w = 0.5 * p.dt / nsub;
 
@@ -57,13 +59,13 @@ __global__ __launch_bounds__(256) void free_prop_kernel(FreePropParams p) {
         double2 f[4], fc[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            if (c < p.n_chan) { f[c] = sample_ch(p, c, t); fc[c] = c_conj(f[c]); }
+            if (c < sy.n_chan) { f[c] = sample_ch(sy, c, t); fc[c] = c_conj(f[c]); }
         }
         for (int e = tid; e < N2 * N2; e += 256) {
-            double2 v = p.L0[e];
-            for (int c = 0; c < p.n_chan; ++c) {
-                c_fma(v, f[c], p.S[(size_t)c * N2 * N2 + e]);
-                c_fma(v, fc[c], p.T[(size_t)c * N2 * N2 + e]);
+            double2 v = sy.L0[e];
+            for (int c = 0; c < sy.n_chan; ++c) {
+                c_fma(v, f[c], sy.S[(size_t)c * N2 * N2 + e]);
+                c_fma(v, fc[c], sy.T[(size_t)c * N2 * N2 + e]);
             }
             A[e] = c_scale(v, w);
         }
@@ -120,7 +122,7 @@ __global__ __launch_bounds__(256) void free_prop_kernel(FreePropParams p) {
         }
         __syncthreads();
     }
-    double2* out = p.M + (size_t)m * N2 * N2;
+    double2* out = p.M + ((size_t)si * 2 * p.n_steps + m) * N2 * N2;
     for (int e = tid; e < N2 * N2; e += 256) out[e] = Acc[e];
 }
 
@@ -134,7 +136,7 @@ hipError_t launch_fp(const FreePropParams& p, hipStream_t s) {
         if (e != hipSuccess) return e;
         attr = true;
     }
-    const int nblk = 2 * p.n_steps;
+    const int nblk = 2 * p.n_steps * p.n_sys;
     if (nblk <= 0) return hipSuccess;
     hipLaunchKernelGGL(free_prop_kernel<N2>, dim3(nblk), dim3(256), lds, s, p);
     return hipGetLastError();

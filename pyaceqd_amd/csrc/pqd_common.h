@@ -30,16 +30,21 @@ __device__ __forceinline__ double2 c_shfl_xor(double2 v, int m) {
 // ---------------------------------------------------------------------------------------------
 // kernel parameter blocks (passed by value)
 // ---------------------------------------------------------------------------------------------
-struct FreePropParams {
+struct FreePropSys {           // one system of a (possibly multi-system) plan
     const double2* L0;       // N2*N2 constant Liouvillian (H0 commutator + dissipators), row-major
     const double2* S;        // n_chan*N2*N2 superoperator of -i/hbar [X_p, .]
     const double2* T;        // n_chan*N2*N2 superoperator of -i/hbar [X_p^dagger, .]
     const double2* samples;  // n_chan*n_samples
     int n_chan, n_samples;
     double s_t0, s_dt;
+};
+
+struct FreePropParams {
+    const FreePropSys* systems;  // device table, n_sys entries
+    int n_sys;
     double ta, dt;
     int n_steps, n_sub;
-    double2* M;              // out: 2*n_steps*N2*N2
+    double2* M;              // out: n_sys*2*n_steps*N2*N2
 };
 
 struct SweepParams {
@@ -54,8 +59,11 @@ struct SweepParams {
     const double2* rho0;     // N2 (row-major vec)
     int n_out;
     const double2* ovec;     // n_out*N2: ovec[k][i*N+j] = O_k[j][i]  => <O_k> = sum_a ovec[k][a] r[a]
-    const int* blk_traj;     // n_blocks*4 trajectory ids (-1: empty slot)
+    const int* blk_traj;     // n_blocks*BT trajectory ids (-1: empty slot)
     const int* blk_end;      // n_blocks: last step of the block (max out_end)
+    const int* blk_sys;      // n_blocks: system of the block (all its trajectories share it)
+    const int* traj_sys;     // n_traj: system of each trajectory (chi = 1 kernel)
+    long long m_stride;      // complex elements between the free propagators of consecutive systems
     const int* wbeg;         // per trajectory
     const int* wend;
     const long long* woff;
@@ -100,7 +108,8 @@ struct FourTimeParams {
 
 // launchers (defined in the .hip translation units)
 hipError_t launch_free_prop(int N2, const FreePropParams& p, hipStream_t s);
-hipError_t launch_sweep(int N2, int CHI, int n_blocks, const SweepParams& p, hipStream_t s);
+hipError_t launch_sweep(int N2, int CHI, int BT, int n_blocks, const SweepParams& p, hipStream_t s);
+int sweep_max_bt(int N2);
 hipError_t launch_sweep_nopt(int N2, int n_blocks, const SweepParams& p, hipStream_t s);
 hipError_t launch_mapchain(const MapChainParams& p, hipStream_t s);
 hipError_t launch_four_time(const FourTimeParams& p, hipStream_t s);

@@ -200,10 +200,11 @@ struct pqd_pt {
 
 struct pqd_plan {
     pqd_ctx* ctx = nullptr;
-    int N2 = 0, CHI = 1, n_traj = 0, n_blocks = 0, n_steps = 0, n_chan = 0;
+    int N2 = 0, CHI = 1, BT = 4, n_traj = 0, n_blocks = 0, n_steps = 0, n_sys = 1;
     bool nopt = true;
-    DevBuf<double2> L0, S, T, samples, M, rho0, ovec, sop, out, cl_ones;
-    DevBuf<int> sched, blk_traj, blk_end, wbeg, wend, ev_start;
+    DevBuf<double2> L0, S, T, samples, M, rho0, ovec, sop, out;
+    DevBuf<FreePropSys> systab;
+    DevBuf<int> sched, blk_traj, blk_end, blk_sys, traj_sys, wbeg, wend, ev_start;
     DevBuf<long long> woff;
     DevBuf<int4> ev;
     FreePropParams fp{};
@@ -212,6 +213,47 @@ struct pqd_plan {
     std::vector<hipEvent_t> evs;  // triplets per execute
     int32_t execs = 0;
 };
+
+
+// upload the generators of n_sys systems into concatenated device buffers + a device table
+static int upload_systems(int n_sys, const pqd_system* systems, hipStream_t s, DevBuf<double2>& L0,
+                          DevBuf<double2>& S, DevBuf<double2>& T, DevBuf<double2>& smp, DevBuf<FreePropSys>& tab) {
+    const int N = systems[0].dim, N2 = N * N;
+    const size_t m2 = (size_t)N2 * N2;
+    std::vector<Generators> G(n_sys);
+    size_t nS = 0, nT = 0, nsmp = 0;
+    for (int k = 0; k < n_sys; ++k) {
+        build_generators(&systems[k], G[k]);
+        nS += G[k].S.size(); nT += G[k].T.size(); nsmp += G[k].samples.size();
+    }
+    std::vector<cd> l0((size_t)n_sys * m2), sv, tv, sm;
+    sv.reserve(nS); tv.reserve(nT); sm.reserve(nsmp);
+    std::vector<size_t> oS, oT, oM;
+    for (int k = 0; k < n_sys; ++k) {
+        std::copy(G[k].L0.begin(), G[k].L0.end(), l0.begin() + k * m2);
+        oS.push_back(sv.size()); sv.insert(sv.end(), G[k].S.begin(), G[k].S.end());
+        oT.push_back(tv.size()); tv.insert(tv.end(), G[k].T.begin(), G[k].T.end());
+        oM.push_back(sm.size()); sm.insert(sm.end(), G[k].samples.begin(), G[k].samples.end());
+    }
+    HIPCHK(L0.upload(reinterpret_cast<double2*>(l0.data()), l0.size(), s));
+    HIPCHK(S.upload(reinterpret_cast<double2*>(sv.data()), sv.size(), s));
+    HIPCHK(T.upload(reinterpret_cast<double2*>(tv.data()), tv.size(), s));
+    HIPCHK(smp.upload(reinterpret_cast<double2*>(sm.data()), sm.size(), s));
+    std::vector<FreePropSys> t(n_sys);
+    for (int k = 0; k < n_sys; ++k) {
+        const pqd_system& y = systems[k];
+        t[k].L0 = L0.p + k * m2;
+        t[k].S = S.p + oS[k];
+        t[k].T = T.p + oT[k];
+        t[k].samples = smp.p + oM[k];
+        t[k].n_chan = y.n_chan;
+        t[k].n_samples = std::max(1, y.n_samples);
+        t[k].s_t0 = y.sample_t0;
+        t[k].s_dt = y.n_chan > 0 ? y.sample_dt : 1.0;
+    }
+    HIPCHK(tab.upload(t.data(), t.size(), s));
+    return PQD_OK;
+}
 
 extern "C" {
 
@@ -302,20 +344,14 @@ int pqd_free_propagators(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* gr
     if ((rc = check_grid(grid))) return rc;
     HIPCHK(hipSetDevice(ctx->device));
     const int N2 = sys->dim * sys->dim;
-    Generators G;
-    build_generators(sys, G);
     DevBuf<double2> L0, S, T, smp, M;
+    DevBuf<FreePropSys> tab;
     hipStream_t s = ctx->stream;
-    HIPCHK(L0.upload(reinterpret_cast<double2*>(G.L0.data()), G.L0.size(), s));
-    HIPCHK(S.upload(reinterpret_cast<double2*>(G.S.data()), G.S.size(), s));
-    HIPCHK(T.upload(reinterpret_cast<double2*>(G.T.data()), G.T.size(), s));
-    HIPCHK(smp.upload(reinterpret_cast<double2*>(G.samples.data()), G.samples.size(), s));
+    if ((rc = upload_systems(1, sys, s, L0, S, T, smp, tab))) return rc;
     const size_t nM = (size_t)2 * grid->n_steps * N2 * N2;
     HIPCHK(M.alloc(nM));
     FreePropParams fp{};
-    fp.L0 = L0.p; fp.S = S.p; fp.T = T.p; fp.samples = smp.p;
-    fp.n_chan = sys->n_chan; fp.n_samples = std::max(1, sys->n_samples);
-    fp.s_t0 = sys->sample_t0; fp.s_dt = sys->n_chan > 0 ? sys->sample_dt : 1.0;
+    fp.systems = tab.p; fp.n_sys = 1;
     fp.ta = grid->ta; fp.dt = grid->dt; fp.n_steps = grid->n_steps; fp.n_sub = grid->n_sub; fp.M = M.p;
     HIPCHK(launch_free_prop(N2, fp, s));
     if (nM) HIPCHK(hipMemcpyAsync(M_out, M.p, nM * sizeof(double2), hipMemcpyDeviceToHost, s));
@@ -323,12 +359,21 @@ int pqd_free_propagators(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* gr
     return PQD_OK;
 }
 
-int pqd_plan_create(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* grid, const pqd_pt* pt,
-                    const int32_t* sched, const pqd_c128* rho0, int32_t n_out, const pqd_c128* out_ops,
-                    const pqd_traj* tr, int64_t out_len, pqd_plan** out) {
-    if (!ctx || !rho0 || !tr || !out) return fail(PQD_ERR_ARG, "NULL argument");
-    int rc = check_system(sys);
-    if (rc) return rc;
+int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems, const int32_t* traj_sys,
+                          const pqd_grid* grid, const pqd_pt* pt, const int32_t* sched, const pqd_c128* rho0,
+                          int32_t n_out, const pqd_c128* out_ops, const pqd_traj* tr, int64_t out_len,
+                          pqd_plan** out) {
+    if (!ctx || !rho0 || !tr || !out || !systems) return fail(PQD_ERR_ARG, "NULL argument");
+    if (n_sys < 1) return fail(PQD_ERR_ARG, "n_sys must be >= 1");
+    if (n_sys > 1 && !traj_sys) return fail(PQD_ERR_ARG, "traj_sys is NULL with n_sys > 1");
+    int rc = 0;
+    for (int k = 0; k < n_sys; ++k) {
+        if ((rc = check_system(&systems[k]))) return rc;
+        if (systems[k].dim != systems[0].dim) return fail(PQD_ERR_ARG, "system %d: dim %d != %d", k, systems[k].dim, systems[0].dim);
+    }
+    const pqd_system* sys = systems;
+    for (int t = 0; t < tr->n_traj; ++t)
+        if (traj_sys && (traj_sys[t] < 0 || traj_sys[t] >= n_sys)) return fail(PQD_ERR_ARG, "traj_sys[%d]=%d out of [0,%d)", t, traj_sys[t], n_sys);
     if ((rc = check_grid(grid))) return rc;
     const int N = sys->dim, N2 = N * N;
     const size_t m2 = (size_t)N2 * N2;
@@ -372,16 +417,14 @@ int pqd_plan_create(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* grid, c
     P->ctx = ctx; P->N2 = N2; P->n_traj = tr->n_traj; P->n_steps = ns; P->out_len = out_len;
     P->nopt = (pt == nullptr);
     P->CHI = pt ? pt->CHI : 1;
-    P->n_chan = sys->n_chan;
+    P->n_sys = n_sys;
 
-    // ---- generators for the free propagators
-    Generators G;
-    build_generators(sys, G);
-    HIPCHK(P->L0.upload(reinterpret_cast<double2*>(G.L0.data()), G.L0.size(), s));
-    HIPCHK(P->S.upload(reinterpret_cast<double2*>(G.S.data()), G.S.size(), s));
-    HIPCHK(P->T.upload(reinterpret_cast<double2*>(G.T.data()), G.T.size(), s));
-    HIPCHK(P->samples.upload(reinterpret_cast<double2*>(G.samples.data()), G.samples.size(), s));
-    HIPCHK(P->M.alloc(std::max<size_t>(1, (size_t)2 * ns * m2)));
+    // ---- generators for the free propagators (one table entry per system)
+    if ((rc = upload_systems(n_sys, systems, s, P->L0, P->S, P->T, P->samples, P->systab))) return rc;
+    HIPCHK(P->M.alloc(std::max<size_t>(1, (size_t)n_sys * 2 * ns * m2)));
+    std::vector<int> tsys(std::max(1, tr->n_traj), 0);
+    for (int t = 0; t < tr->n_traj; ++t) tsys[t] = traj_sys ? traj_sys[t] : 0;
+    HIPCHK(P->traj_sys.upload(tsys.data(), tsys.size(), s));
 
     // ---- MTO events: per trajectory, stable-sorted by (step, phase), same-slot ops composed
     std::vector<std::vector<int>> per(tr->n_traj);
@@ -431,23 +474,45 @@ int pqd_plan_create(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* grid, c
     HIPCHK(P->woff.upload(reinterpret_cast<const long long*>(tr->out_offset), std::max(1, tr->n_traj), s));
     std::vector<int> order(tr->n_traj);
     for (int t = 0; t < tr->n_traj; ++t) order[t] = t;
-    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return tr->out_end[a] > tr->out_end[b]; });
-    const int nb = (tr->n_traj + 3) / 4;
-    std::vector<int> bt(std::max(1, nb * 4), -1), be(std::max(1, nb), 0);
-    for (int k = 0; k < tr->n_traj; ++k) {
-        bt[k] = order[k];
-        be[k / 4] = std::max(be[k / 4], tr->out_end[order[k]]);
+    // group by system (a workgroup shares one set of free propagators), longest first inside a system
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+        if (tsys[a] != tsys[b]) return tsys[a] < tsys[b];
+        return tr->out_end[a] > tr->out_end[b];
+    });
+    // trajectories per workgroup: 8 (half the PT-slice L2 traffic per trajectory) when the LDS allows it
+    // and the batch still fills every CU, else 4
+    int n_cu = 256;
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess) n_cu = prop.multiProcessorCount;
     }
+    int BT = (sweep_max_bt(N2) >= 8 && tr->n_traj >= 8 * n_cu) ? 8 : 4;
+    if (const char* e = getenv("PQD_BT")) BT = std::min(atoi(e) >= 8 ? 8 : 4, sweep_max_bt(N2));
+    P->BT = BT;
+    std::vector<int> bt, be, bs;
+    for (size_t k = 0; k < order.size();) {  // blocks never mix systems
+        const int sy = tsys[order[k]];
+        int filled = 0, end = 0;
+        while (k < order.size() && filled < BT && tsys[order[k]] == sy) {
+            bt.push_back(order[k]);
+            end = std::max(end, tr->out_end[order[k]]);
+            ++k; ++filled;
+        }
+        for (; filled < BT; ++filled) bt.push_back(-1);
+        be.push_back(end);
+        bs.push_back(sy);
+    }
+    const int nb = (int)be.size();
+    if (bt.empty()) { bt.assign(BT, -1); be.assign(1, 0); bs.assign(1, 0); }
     P->n_blocks = nb;
     HIPCHK(P->blk_traj.upload(bt.data(), bt.size(), s));
     HIPCHK(P->blk_end.upload(be.data(), be.size(), s));
+    HIPCHK(P->blk_sys.upload(bs.data(), bs.size(), s));
     HIPCHK(P->sched.upload(sch.data(), sch.size(), s));
     HIPCHK(P->out.alloc(std::max<int64_t>(1, out_len)));
     HIPCHK(hipMemsetAsync(P->out.p, 0, std::max<int64_t>(1, out_len) * sizeof(double2), s));
 
-    P->fp.L0 = P->L0.p; P->fp.S = P->S.p; P->fp.T = P->T.p; P->fp.samples = P->samples.p;
-    P->fp.n_chan = sys->n_chan; P->fp.n_samples = std::max(1, sys->n_samples);
-    P->fp.s_t0 = sys->sample_t0; P->fp.s_dt = sys->n_chan > 0 ? sys->sample_dt : 1.0;
+    P->fp.systems = P->systab.p; P->fp.n_sys = n_sys;
     P->fp.ta = grid->ta; P->fp.dt = grid->dt; P->fp.n_steps = ns; P->fp.n_sub = grid->n_sub; P->fp.M = P->M.p;
 
     SweepParams& sp = P->sp;
@@ -457,12 +522,19 @@ int pqd_plan_create(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* grid, c
         sp.bond0 = pt->bond0.p; sp.gmap = pt->gmap.p;
     }
     sp.sched = P->sched.p; sp.rho0 = P->rho0.p; sp.n_out = n_out; sp.ovec = P->ovec.p;
-    sp.blk_traj = P->blk_traj.p; sp.blk_end = P->blk_end.p; sp.wbeg = P->wbeg.p; sp.wend = P->wend.p;
+    sp.blk_traj = P->blk_traj.p; sp.blk_end = P->blk_end.p; sp.blk_sys = P->blk_sys.p;
+    sp.traj_sys = P->traj_sys.p; sp.m_stride = (long long)2 * ns * m2; sp.wbeg = P->wbeg.p; sp.wend = P->wend.p;
     { const char* ab = getenv("PQD_ABLATE"); sp.ablate = ab ? atoi(ab) : 0; }
     sp.woff = P->woff.p; sp.ev_start = P->ev_start.p; sp.ev = P->ev.p; sp.sop = P->sop.p; sp.out = P->out.p;
     HIPCHK(hipStreamSynchronize(s));
     *out = guard.release();
     return PQD_OK;
+}
+
+int pqd_plan_create(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* grid, const pqd_pt* pt,
+                    const int32_t* sched, const pqd_c128* rho0, int32_t n_out, const pqd_c128* out_ops,
+                    const pqd_traj* tr, int64_t out_len, pqd_plan** out) {
+    return pqd_plan_create_multi(ctx, 1, sys, nullptr, grid, pt, sched, rho0, n_out, out_ops, tr, out_len, out);
 }
 
 int pqd_plan_execute(pqd_plan* P, int32_t rebuild_free) {
@@ -477,7 +549,7 @@ int pqd_plan_execute(pqd_plan* P, int32_t rebuild_free) {
     if (P->nopt)
         HIPCHK(launch_sweep_nopt(P->N2, P->n_traj, P->sp, s));
     else
-        HIPCHK(launch_sweep(P->N2, P->CHI, P->n_blocks, P->sp, s));
+        HIPCHK(launch_sweep(P->N2, P->CHI, P->BT, P->n_blocks, P->sp, s));
     HIPCHK(hipEventRecord(e[2], s));
     for (int i = 0; i < 3; ++i) P->evs.push_back(e[i]);
     P->execs++;
@@ -529,8 +601,15 @@ void pqd_plan_destroy(pqd_plan* P) {
 int pqd_propagate(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* grid, const pqd_pt* pt,
                   const int32_t* sched, const pqd_c128* rho0, int32_t n_out, const pqd_c128* out_ops,
                   const pqd_traj* tr, pqd_c128* out, int64_t out_len) {
+    return pqd_propagate_multi(ctx, 1, sys, nullptr, grid, pt, sched, rho0, n_out, out_ops, tr, out, out_len);
+}
+
+int pqd_propagate_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems, const int32_t* traj_sys,
+                        const pqd_grid* grid, const pqd_pt* pt, const int32_t* sched, const pqd_c128* rho0,
+                        int32_t n_out, const pqd_c128* out_ops, const pqd_traj* tr, pqd_c128* out,
+                        int64_t out_len) {
     pqd_plan* P = nullptr;
-    int rc = pqd_plan_create(ctx, sys, grid, pt, sched, rho0, n_out, out_ops, tr, out_len, &P);
+    int rc = pqd_plan_create_multi(ctx, n_sys, systems, traj_sys, grid, pt, sched, rho0, n_out, out_ops, tr, out_len, &P);
     if (rc) return rc;
     rc = pqd_plan_execute(P, 1);
     if (!rc) rc = pqd_plan_download(P, out, out_len);

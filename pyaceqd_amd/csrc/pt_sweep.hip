@@ -26,9 +26,7 @@
 
 namespace {
 
-constexpr int BT = 4;  // trajectories per workgroup
-
-template <int N2, int CHI>
+template <int N2, int CHI, int BT>
 struct SweepLayout {
     static constexpr int RS = CHI + 1;          // row stride (double2)
     static constexpr int TS = N2 * RS + 4;      // trajectory stride (+64 B: shifts banks per trajectory)
@@ -52,11 +50,12 @@ __device__ __forceinline__ void col_apply(const double2* __restrict__ Op, double
     }
 }
 
-template <int N2, int CHI>
-__global__ __launch_bounds__(256) void pt_sweep_kernel(SweepParams p, const double2* __restrict__ Mg,
-                                                       const double2* __restrict__ Qg0, double2* __restrict__ outg) {
-    using L = SweepLayout<N2, CHI>;
+template <int N2, int CHI, int BT>
+__global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const double2* __restrict__ Mg,
+                                                           const double2* __restrict__ Qg0, double2* __restrict__ outg) {
+    using L = SweepLayout<N2, CHI, BT>;
     constexpr int RS = L::RS, TS = L::TS, KD = L::KD, NCOL = L::NCOL;
+    constexpr int NT = 64 * BT, NW = BT;  // threads, waves
     extern __shared__ __attribute__((aligned(16))) double2 smem[];
     double2* st = smem;
     double2* rbuf = smem + BT * TS;
@@ -76,6 +75,7 @@ __global__ __launch_bounds__(256) void pt_sweep_kernel(SweepParams p, const doub
     }
     __syncthreads();
     const int n_end = p.blk_end[blockIdx.x];
+    Mg += (size_t)p.blk_sys[blockIdx.x] * p.m_stride;
 
     // ---- column-phase ownership: thread -> column (cb, cd)
     const bool colthr = tid < NCOL;
@@ -106,8 +106,8 @@ __global__ __launch_bounds__(256) void pt_sweep_kernel(SweepParams p, const doub
         if (need && !(p.ablate & 4)) {
             const double2* cvec = (n == 0) ? p.closure0 : p.closure + (size_t)p.sched[n - 1] * CHI;
             constexpr int NPART = BT * N2 * 4;
-            for (int it = 0; it < (NPART + 255) / 256; ++it) {
-                const int e = tid + 256 * it;
+            for (int it = 0; it < (NPART + NT - 1) / NT; ++it) {
+                const int e = tid + NT * it;
                 const int row = e >> 2, qr = e & 3;
                 double2 s = c_zero();
                 if (e < NPART) {
@@ -121,7 +121,7 @@ __global__ __launch_bounds__(256) void pt_sweep_kernel(SweepParams p, const doub
                 if (e < NPART && qr == 0) rbuf[row] = s;
             }
             __syncthreads();
-            for (int e = tid; e < BT * p.n_out; e += 256) {
+            for (int e = tid; e < BT * p.n_out; e += NT) {
                 const int b = e / p.n_out, k = e - (e / p.n_out) * p.n_out;
                 if (s_wb[b] <= n && n <= s_we[b]) {
                     double2 s = c_zero();
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256) void pt_sweep_kernel(SweepParams p, const doub
         // ------------------------------------------------------------ PT contraction
         if (!(p.ablate & 1)) {
             const double2* Qs = Qg0 + (size_t)p.sched[n] * p.D * CHI * CHI;
-            for (int a = wave; a < N2; a += 4) {
+            for (int a = wave; a < N2; a += NW) {
                 const double2* Qg = Qs + (size_t)p.gmap[a] * CHI * CHI + pj;
                 const double2* xr = st + a * RS + pq;
                 double2 acc[BT][KD];
@@ -282,7 +282,7 @@ __global__ __launch_bounds__(64) void sweep_nopt_kernel(SweepParams p) {
             own = lane_apply<N2>(p.sop + (size_t)e.z * N2 * N2, own, lane);
             ++ev_cur;
         }
-        const double2* Ma = p.M + (size_t)(2 * n) * N2 * N2;
+        const double2* Ma = p.M + (size_t)p.traj_sys[t] * p.m_stride + (size_t)(2 * n) * N2 * N2;
         own = lane_apply<N2>(Ma, own, lane);
         own = lane_apply<N2>(Ma + N2 * N2, own, lane);
         while (ev_cur < ev_lim) {
@@ -294,27 +294,27 @@ __global__ __launch_bounds__(64) void sweep_nopt_kernel(SweepParams p) {
     }
 }
 
-template <int N2, int CHI>
+template <int N2, int CHI, int BT>
 hipError_t launch_sw(int n_blocks, const SweepParams& p, hipStream_t s) {
-    using L = SweepLayout<N2, CHI>;
+    using L = SweepLayout<N2, CHI, BT>;
     static_assert(L::LDS <= 160 * 1024, "LDS budget");
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)pt_sweep_kernel<N2, CHI>,
+        hipError_t e = hipFuncSetAttribute((const void*)pt_sweep_kernel<N2, CHI, BT>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::LDS);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((pt_sweep_kernel<N2, CHI>), dim3(n_blocks), dim3(256), L::LDS, s, p, p.M, p.Q, p.out);
+    hipLaunchKernelGGL((pt_sweep_kernel<N2, CHI, BT>), dim3(n_blocks), dim3(64 * BT), L::LDS, s, p, p.M, p.Q, p.out);
     return hipGetLastError();
 }
 
-template <int N2>
+template <int N2, int BT>
 hipError_t launch_sw_chi(int CHI, int n_blocks, const SweepParams& p, hipStream_t s) {
     switch (CHI) {
-        case 16: return launch_sw<N2, 16>(n_blocks, p, s);
-        case 32: return launch_sw<N2, 32>(n_blocks, p, s);
-        case 64: return launch_sw<N2, 64>(n_blocks, p, s);
+        case 16: return launch_sw<N2, 16, BT>(n_blocks, p, s);
+        case 32: return launch_sw<N2, 32, BT>(n_blocks, p, s);
+        case 64: return launch_sw<N2, 64, BT>(n_blocks, p, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -326,14 +326,26 @@ bool sweep_supported(int N2, int CHI) {
            (CHI == 1 || CHI == 16 || CHI == 32 || CHI == 64);
 }
 
-hipError_t launch_sweep(int N2, int CHI, int n_blocks, const SweepParams& p, hipStream_t s) {
+// trajectories per workgroup that fit the LDS for this N2 (8 halves the per-trajectory PT-slice traffic)
+int sweep_max_bt(int N2) { return N2 <= 16 ? 8 : 4; }
+
+hipError_t launch_sweep(int N2, int CHI, int BT, int n_blocks, const SweepParams& p, hipStream_t s) {
     if (n_blocks <= 0) return hipSuccess;
+    if (BT == 8) {
+        switch (N2) {
+            case 4: return launch_sw_chi<4, 8>(CHI, n_blocks, p, s);
+            case 9: return launch_sw_chi<9, 8>(CHI, n_blocks, p, s);
+            case 16: return launch_sw_chi<16, 8>(CHI, n_blocks, p, s);
+            default: return hipErrorInvalidValue;
+        }
+    }
+    if (BT != 4) return hipErrorInvalidValue;
     switch (N2) {
-        case 4: return launch_sw_chi<4>(CHI, n_blocks, p, s);
-        case 9: return launch_sw_chi<9>(CHI, n_blocks, p, s);
-        case 16: return launch_sw_chi<16>(CHI, n_blocks, p, s);
-        case 25: return launch_sw_chi<25>(CHI, n_blocks, p, s);
-        case 36: return launch_sw_chi<36>(CHI, n_blocks, p, s);
+        case 4: return launch_sw_chi<4, 4>(CHI, n_blocks, p, s);
+        case 9: return launch_sw_chi<9, 4>(CHI, n_blocks, p, s);
+        case 16: return launch_sw_chi<16, 4>(CHI, n_blocks, p, s);
+        case 25: return launch_sw_chi<25, 4>(CHI, n_blocks, p, s);
+        case 36: return launch_sw_chi<36, 4>(CHI, n_blocks, p, s);
         default: return hipErrorInvalidValue;
     }
 }

@@ -162,6 +162,7 @@ class Trajectories:
     out_begin: np.ndarray
     out_end: np.ndarray
     mtos: List[MTO] = field(default_factory=list)
+    system: Optional[np.ndarray] = None   # per-trajectory index into a list of systems (scans)
 
     @property
     def n_traj(self):
@@ -205,9 +206,18 @@ def split_output(out, traj, n_out):
     return res
 
 
+def _systems(system):
+    return list(system) if isinstance(system, (list, tuple)) else [system]
+
+
 def _prep(system, grid, rho0, out_ops, traj, pt, ctx):
-    N = system.dim
-    sc, k1 = system.to_c()
+    systems = _systems(system)
+    N = systems[0].dim
+    if any(s.dim != N for s in systems):
+        raise ValueError("all systems of a batch must have the same dimension")
+    convs = [s.to_c() for s in systems]
+    sc = (_lib.pqd_system * len(systems))(*[c for c, _ in convs])
+    k1 = [k for _, k in convs]
     gc = grid.to_c()
     r0 = _c(rho0).reshape(N * N)
     ops = _c(np.stack([np.asarray(o).reshape(N, N) for o in out_ops]))
@@ -219,22 +229,27 @@ def _prep(system, grid, rho0, out_ops, traj, pt, ctx):
             raise ValueError(f"PT gmap has {pt.gmap.shape[0]} entries, system needs {N * N}")
         pth = pt.handle(ctx, N)
         sched = pt.schedule(max(1, grid.n_steps))
-    keep = (k1, k2, r0, ops, sched, sc, gc, tc)
+    tsys = np.ascontiguousarray(np.zeros(max(1, traj.n_traj)) if traj.system is None else traj.system, dtype=np.int32)
+    if len(systems) == 1 and traj.system is not None and np.any(tsys != 0):
+        raise ValueError("trajectory system index out of range")
+    keep = (k1, k2, r0, ops, sched, sc, gc, tc, tsys, len(systems))
     return keep, total
 
 
-def propagate(system: System, grid: Grid, rho0, out_ops: Sequence, traj: Trajectories,
+def propagate(system, grid: Grid, rho0, out_ops: Sequence, traj: Trajectories,
               pt: Optional[ProcessTensor] = None, ctx=None):
-    """Run all trajectories; returns a list of (window_len, n_out) complex arrays."""
+    """Run all trajectories; returns a list of (window_len, n_out) complex arrays.
+    `system` may be a list of Systems (parameter scan); traj.system then selects one per trajectory."""
     ctx = ctx or _lib.context()
+    dim = _systems(system)[0].dim
     with ctx.lock:
         keep, total = _prep(system, grid, rho0, out_ops, traj, pt, ctx)
-        k1, k2, r0, ops, sched, sc, gc, tc = keep
+        k1, k2, r0, ops, sched, sc, gc, tc, tsys, n_sys = keep
         out = np.zeros(max(1, total), dtype=np.complex128)
-        pth = pt.handle(ctx, system.dim) if pt is not None else None
-        _lib.check(_lib.lib().pqd_propagate(ctx.handle, C.byref(sc), C.byref(gc), pth, _lib.iptr(sched),
-                                            _lib.cptr(r0), len(out_ops), _lib.cptr(ops), C.byref(tc),
-                                            _lib.cptr(out), max(1, total)))
+        pth = pt.handle(ctx, dim) if pt is not None else None
+        _lib.check(_lib.lib().pqd_propagate_multi(ctx.handle, n_sys, sc, _lib.iptr(tsys), C.byref(gc), pth,
+                                                  _lib.iptr(sched), _lib.cptr(r0), len(out_ops), _lib.cptr(ops),
+                                                  C.byref(tc), _lib.cptr(out), max(1, total)))
     return split_output(out, traj, len(out_ops))
 
 
@@ -257,15 +272,16 @@ class Plan:
         self.ctx = ctx or _lib.context()
         self.traj = traj
         self.n_out = len(out_ops)
-        self.dim = system.dim
+        self.dim = _systems(system)[0].dim
         with self.ctx.lock:
             self._keep, self.total = _prep(system, grid, rho0, out_ops, traj, pt, self.ctx)
-            k1, k2, r0, ops, sched, sc, gc, tc = self._keep
-            pth = pt.handle(self.ctx, system.dim) if pt is not None else None
+            k1, k2, r0, ops, sched, sc, gc, tc, tsys, n_sys = self._keep
+            pth = pt.handle(self.ctx, self.dim) if pt is not None else None
             h = C.c_void_p()
-            _lib.check(_lib.lib().pqd_plan_create(self.ctx.handle, C.byref(sc), C.byref(gc), pth, _lib.iptr(sched),
-                                                  _lib.cptr(r0), self.n_out, _lib.cptr(ops), C.byref(tc),
-                                                  max(1, self.total), C.byref(h)))
+            _lib.check(_lib.lib().pqd_plan_create_multi(self.ctx.handle, n_sys, sc, _lib.iptr(tsys), C.byref(gc),
+                                                        pth, _lib.iptr(sched), _lib.cptr(r0), self.n_out,
+                                                        _lib.cptr(ops), C.byref(tc), max(1, self.total),
+                                                        C.byref(h)))
             self.handle = h
         self._pt = pt
 

@@ -27,7 +27,7 @@ def _work(block):
     from oracle import oracle
     out = []
     for e0 in block:
-        sysd, grid, pt, rho0, ops, tr = bench.build_workload(2, 30, 16, rank=int(round((e0 - 1.0) / 0.1)))
+        sysd, grid, pt, rho0, ops, tr = bench.build_workload(2, 30, 16, scan_offset=int(round((e0 - 1.0) / 0.05)))
         r = oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt)
         out.append(np.concatenate([x.ravel() for x in r]))
     return out
@@ -52,7 +52,7 @@ def _free_port():
 
 
 def test_gloo_world2_scan_matches_single_process():
-    units = [1.0 + 0.1 * k for k in range(5)]
+    units = [1.0 + 0.05 * k for k in range(5)]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

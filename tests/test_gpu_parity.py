@@ -294,3 +294,42 @@ def test_calc_dynmap_consistency():
     assert np.max(np.abs(res - direct)) < 1e-12
     rho_end = (dm[-1] @ rho0.reshape(4)).reshape(2, 2)
     assert abs(rho_end[1, 1] - direct[2][-1]) < 1e-12
+
+
+# --------------------------------------------------------------------------------- B = 8 workgroups, scans
+@pytest.mark.parametrize("N", [2, 3, 4])
+@pytest.mark.parametrize("chi", [16, 32, 64])
+def test_sweep_pt_bt8(monkeypatch, N, chi):
+    monkeypatch.setenv("PQD_BT", "8")
+    sysd, grid = H.random_system(N, n_steps=20, seed=5 * N + chi)
+    pt = ptmod.random_pt(N, chi, D=min(N * N, 7), n_slices=9, seed=chi + 1, eps=0.15)
+    tr = _traj(grid.n_steps, N, 19, seed=N + chi)
+    ops = [H.ketbra(N, 0, 0), H.ketbra(N, 1, 0), np.eye(N)]
+    rho0 = H.random_rho(N)
+    cmp_lists(engine.propagate(sysd, grid, rho0, ops, tr, pt=pt),
+              oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
+
+
+@pytest.mark.parametrize("with_pt", [False, True])
+def test_multi_system_scan(with_pt):
+    N = 4
+    systems = [H.random_system(N, n_steps=30, seed=20 + k)[0] for k in range(3)]
+    grid = Grid(0.0, 0.1, 30)
+    tr = _traj(grid.n_steps, N, 13, seed=9)
+    tr.system = np.array([k % 3 for k in range(13)])
+    pt = ptmod.random_pt(N, 32, D=9, n_slices=5, seed=3, eps=0.1) if with_pt else None
+    ops = [H.ketbra(N, 1, 1), H.ketbra(N, 3, 0)]
+    rho0 = H.random_rho(N)
+    cmp_lists(engine.propagate(systems, grid, rho0, ops, tr, pt=pt),
+              oracle.propagate(systems, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
+
+
+def test_bench_workload_small_vs_oracle():
+    """the bench workload itself (scan of G2 sweeps, chi=64, B=8 path) at reduced n_tau vs the oracle"""
+    import bench
+    systems, grid, pt, rho0, ops, tr = bench.build_workload(16, 60, 64, scan=2)
+    plan = engine.Plan(systems, grid, rho0, ops, tr, pt=pt)
+    plan.execute()
+    got = plan.download()
+    ref = oracle.propagate(systems, grid, rho0, ops, tr, pt=pt, nthreads=8)
+    cmp_lists(got, ref, 1e-11)
