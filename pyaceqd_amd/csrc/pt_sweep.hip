@@ -10,9 +10,9 @@
 //     steps, no inter-workgroup traffic at all: trajectories are independent);
 //   * the 4 augmented states Q_b[alpha][d] (N2 x CHI complex doubles, 16 KiB each at N=4, chi=64)
 //     stay resident in LDS, rows padded to CHI+1 so column reads and row reads are bank-conflict free;
-//   * free half steps (N2 x N2 propagator applied to every bond column): one thread per column (b, d),
-//     the propagator is wave-uniform and streamed through the scalar cache (s_load), the column sits
-//     in VGPRs — no cross-thread traffic, no barrier inside the phase;
+//   * free half steps (N2 x N2 propagator applied to every bond column): one wave per trajectory runs
+//     the complex GEMM M . Q on the FP64 matrix cores (v_mfma_f64_16x16x4_f64, 4 real MFMAs per
+//     complex tile), no cross-wave traffic, no barrier inside the phase;
 //   * PT contraction (row alpha of all 4 trajectories times the chi x chi slice Q[g(alpha)]): waves
 //     split the alpha rows; lane (j, q) owns output columns {j, j+16, j+32, j+48} and the input
 //     quarter d = 4k + q, so every Q element is read from L2 exactly once per workgroup and feeds
@@ -35,19 +35,66 @@ struct SweepLayout {
     static constexpr size_t LDS = (size_t)(BT * TS + BT * N2) * sizeof(double2);
 };
 
-// column op: col <- Op col   (Op row-major N2 x N2; result written straight back to the LDS column)
-template <int N2, int RS>
-__device__ __forceinline__ void col_apply(const double2* __restrict__ Op, double2* col) {
-    double2 v[N2];
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+// Column phase on the matrix cores: one wave applies the N2 x N2 operator Op (row-major, complex) to
+// all CHI bond columns of its trajectory's augmented state S (LDS, row stride RS):
+//   C[N2 x CHI] = Op[N2 x N2] . S[N2 x CHI]   as v_mfma_f64_16x16x4_f64 tiles,
+// complex = 4 real MFMAs (Cr += Ar Br - Ai Bi, Ci += Ar Bi + Ai Br). Fragment maps (gfx950 f64):
+// A[i = l&15][k = l>>4], B[k = l>>4][j = l&15], C[i = (l>>4) + 4 r][j = l&15].
+// Column tiles are the outer loop, so each 16-column tile is read completely before it is written
+// back in place. Rows/k beyond N2 are zero padding (N2 = 4, 9, 25, 36).
+template <int N2, int CHI, int RS>
+__device__ __forceinline__ void col_apply_mfma(const double2* __restrict__ Op, double2* S, int lane) {
+    constexpr int MT = (N2 + 15) / 16;   // output row tiles
+    constexpr int KS = (N2 + 3) / 4;     // k steps
+    constexpr int NTL = CHI / 16;        // column tiles
+    constexpr bool CACHE_A = KS * MT <= 8;
+    const int li = lane & 15, lk = lane >> 4;
+    double2 ac[CACHE_A ? KS * MT : 1];
+    if constexpr (CACHE_A) {
 #pragma unroll
-    for (int a = 0; a < N2; ++a) v[a] = col[a * RS];
-    for (int r = 0; r < N2; ++r) {
-        const double2* Or = Op + r * N2;
-        double2 acc = c_zero();
+        for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-        for (int a = 0; a < N2; ++a) c_fma(acc, Or[a], v[a]);
-        col[r * RS] = acc;
+            for (int mt = 0; mt < MT; ++mt) {
+                const int r = 16 * mt + li, a = 4 * ks + lk;
+                ac[ks * MT + mt] = (r < N2 && a < N2) ? Op[r * N2 + a] : c_zero();
+            }
     }
+#pragma unroll
+    for (int nt = 0; nt < NTL; ++nt) {
+        dbl4 cr[MT], ci[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) { cr[mt] = dbl4{0, 0, 0, 0}; ci[mt] = dbl4{0, 0, 0, 0}; }
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int a = 4 * ks + lk;
+            const double2 b = (a < N2) ? S[a * RS + 16 * nt + li] : c_zero();
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+                double2 m;
+                if constexpr (CACHE_A) {
+                    m = ac[ks * MT + mt];
+                } else {
+                    const int r = 16 * mt + li;
+                    m = (r < N2 && a < N2) ? Op[r * N2 + a] : c_zero();
+                }
+                cr[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(m.x, b.x, cr[mt], 0, 0, 0);
+                cr[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(-m.y, b.y, cr[mt], 0, 0, 0);
+                ci[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(m.x, b.y, ci[mt], 0, 0, 0);
+                ci[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(m.y, b.x, ci[mt], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 16 * mt + lk + 4 * r;
+                if (row < N2) S[row * RS + 16 * nt + li] = make_double2(cr[mt][r], ci[mt][r]);
+            }
+    }
+    // the next operator of this wave re-reads what other lanes just wrote
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
 template <int N2, int CHI, int BT>
@@ -77,21 +124,24 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
     const int n_end = p.blk_end[blockIdx.x];
     Mg += (size_t)p.blk_sys[blockIdx.x] * p.m_stride;
 
-    // ---- column-phase ownership: thread -> column (cb, cd)
-    const bool colthr = tid < NCOL;
-    const int cb = tid / CHI, cd = tid - (tid / CHI) * CHI;
-    double2* col = st + cb * TS + cd;
-    int ev_cur = 0, ev_lim = 0;
-    if (colthr) {
-        const int t = s_traj[cb];
-        if (t >= 0) { ev_cur = p.ev_start[t]; ev_lim = p.ev_start[t + 1]; }
+    // ---- initial augmented states rho0 (x) bond0 (thread -> column)
+    for (int c = tid; c < NCOL; c += NT) {
+        const int cb = c / CHI, cd = c - (c / CHI) * CHI;
         const double2 b0 = p.bond0[cd];
 #pragma unroll
-        for (int a = 0; a < N2; ++a) col[a * RS] = c_mul(p.rho0[a], b0);
+        for (int a = 0; a < N2; ++a) st[cb * TS + a * RS + cd] = c_mul(p.rho0[a], b0);
+    }
+    __syncthreads();
+    // ---- column phases: wave w owns trajectory w (its free propagators, its MTO events)
+    double2* stw = st + wave * TS;
+    int ev_cur = 0, ev_lim = 0;
+    {
+        const int t = s_traj[wave];
+        if (t >= 0) { ev_cur = p.ev_start[t]; ev_lim = p.ev_start[t + 1]; }
         while (ev_cur < ev_lim) {  // applyBefore-true MTOs at step 0
             const int4 e = p.ev[ev_cur];
             if (e.x != 0 || e.y != 0) break;
-            col_apply<N2, RS>(p.sop + (size_t)e.z * N2 * N2, col);
+            col_apply_mfma<N2, CHI, RS>(p.sop + (size_t)e.z * N2 * N2, stw, lane);
             ++ev_cur;
         }
     }
@@ -135,14 +185,14 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
 
         // ------------------------------------------------------------ column phase A
         const double2* Ma = Mg + (size_t)(2 * n) * N2 * N2;
-        if (colthr && !(p.ablate & 2)) {
+        if (!(p.ablate & 2)) {
             while (ev_cur < ev_lim) {  // applyBefore-false MTOs at step n
                 const int4 e = p.ev[ev_cur];
                 if (e.x != n || e.y != 1) break;
-                col_apply<N2, RS>(p.sop + (size_t)e.z * N2 * N2, col);
+                col_apply_mfma<N2, CHI, RS>(p.sop + (size_t)e.z * N2 * N2, stw, lane);
                 ++ev_cur;
             }
-            col_apply<N2, RS>(Ma, col);
+            col_apply_mfma<N2, CHI, RS>(Ma, stw, lane);
         }
         __syncthreads();
 
@@ -218,12 +268,12 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
 
         // ------------------------------------------------------------ column phase B
         const double2* Mb = Ma + N2 * N2;
-        if (colthr && !(p.ablate & 2)) {
-            col_apply<N2, RS>(Mb, col);
+        if (!(p.ablate & 2)) {
+            col_apply_mfma<N2, CHI, RS>(Mb, stw, lane);
             while (ev_cur < ev_lim) {  // applyBefore-true MTOs at step n+1
                 const int4 e = p.ev[ev_cur];
                 if (e.x != n + 1 || e.y != 0) break;
-                col_apply<N2, RS>(p.sop + (size_t)e.z * N2 * N2, col);
+                col_apply_mfma<N2, CHI, RS>(p.sop + (size_t)e.z * N2 * N2, stw, lane);
                 ++ev_cur;
             }
         }
