@@ -71,6 +71,7 @@ struct SweepParams {
     const int4* ev;          // (step, after?1:0, superop index, 0), sorted per trajectory
     const double2* sop;      // MTO superoperators N2*N2 each
     double2* out;
+    int pt_mode;             // PT contraction: 0 VALU, 1 matrix cores (4x4x4_4b), 2 mixed per wave
     int ablate;              // diagnostics only (PQD_ABLATE): 1 skip PT, 2 skip column phases, 4 skip outputs
 };
 

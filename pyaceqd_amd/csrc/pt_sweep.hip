@@ -97,6 +97,55 @@ __device__ __forceinline__ void col_apply_mfma(const double2* __restrict__ Op, d
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
+// PT contraction of one Liouville row alpha on the matrix cores (v_mfma_f64_4x4x4_4b_f64):
+//   C[BT x CHI] = X[BT x CHI] . Qg[CHI x CHI],  X = rows alpha of the BT trajectories.
+// gfx950 lane map of the 4-block f64 MFMA (measured): lane l = 16 k + 4 blk + x holds A[blk][x][k],
+// B[blk][k][x], D[blk][l>>4][x]. The 4 blocks of one instruction are 4 consecutive 4-column tiles,
+// so lane l reads Qg[4 ks + (l>>4)][16 grp + (l & 15)] (256 contiguous bytes per 16 lanes) and ends up
+// owning C[4 rb + (l>>4)][16 grp + (l & 15)]: no cross-lane reduction. Complex = 4 real MFMAs.
+template <int CHI, int BT, int RS, int TS>
+__device__ __forceinline__ void pt_row_mfma(const double2* __restrict__ Qg, double2* st, int a, int lane) {
+    constexpr int RB = BT / 4, NG = CHI / 16, KSN = CHI / 4;
+    const int x = lane & 3, kk = lane >> 4, c16 = lane & 15;
+    double cr[RB][NG], ci[RB][NG];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int g = 0; g < NG; ++g) { cr[rb][g] = 0.0; ci[rb][g] = 0.0; }
+    const double2* xr = st + a * RS + kk;          // + b*TS + 4 ks
+    const double2* qp = Qg + (size_t)kk * CHI + c16;  // + 4 ks * CHI + 16 g
+    double2 qn[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) qn[g] = qp[16 * g];
+#pragma unroll 2
+    for (int ks = 0; ks < KSN; ++ks) {
+        double2 qv[NG];
+#pragma unroll
+        for (int g = 0; g < NG; ++g) qv[g] = qn[g];
+        if (ks + 1 < KSN) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) qn[g] = qp[(size_t)4 * (ks + 1) * CHI + 16 * g];
+        }
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+            const double2 av = xr[(4 * rb + x) * TS + 4 * ks];
+            const double ai_neg = -av.y;
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                cr[rb][g] = __builtin_amdgcn_mfma_f64_4x4x4f64(av.x, qv[g].x, cr[rb][g], 0, 0, 0);
+                cr[rb][g] = __builtin_amdgcn_mfma_f64_4x4x4f64(ai_neg, qv[g].y, cr[rb][g], 0, 0, 0);
+                ci[rb][g] = __builtin_amdgcn_mfma_f64_4x4x4f64(av.x, qv[g].y, ci[rb][g], 0, 0, 0);
+                ci[rb][g] = __builtin_amdgcn_mfma_f64_4x4x4f64(av.y, qv[g].x, ci[rb][g], 0, 0, 0);
+            }
+        }
+    }
+    double2* wr = st + a * RS + c16;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int g = 0; g < NG; ++g) wr[(4 * rb + kk) * TS + 16 * g] = make_double2(cr[rb][g], ci[rb][g]);
+}
+
 template <int N2, int CHI, int BT>
 __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const double2* __restrict__ Mg,
                                                            const double2* __restrict__ Qg0, double2* __restrict__ outg) {
@@ -199,8 +248,18 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
         // ------------------------------------------------------------ PT contraction
         if (!(p.ablate & 1)) {
             const double2* Qs = Qg0 + (size_t)p.sched[n] * p.D * CHI * CHI;
+            // pt_mode 0: VALU rows, 1: matrix-core rows, 2: mixed (waves 0..NW/2-1 start on the matrix cores,
+            // the others on the VALU, alternating per row), so the two FP64 pipes of a SIMD run concurrently
+            int parity = (p.pt_mode == 2) ? ((wave >= NW / 2) ? 1 : 0) : 0;
             for (int a = wave; a < N2; a += NW) {
-                const double2* Qg = Qs + (size_t)p.gmap[a] * CHI * CHI + pj;
+                const double2* Qg = Qs + (size_t)p.gmap[a] * CHI * CHI;
+                const bool use_mfma = (p.pt_mode == 1) || (p.pt_mode == 2 && parity == 0);
+                parity ^= 1;
+                if (use_mfma) {
+                    pt_row_mfma<CHI, BT, RS, TS>(Qg, st, a, lane);
+                    continue;
+                }
+                Qg += pj;
                 const double2* xr = st + a * RS + pq;
                 double2 acc[BT][KD];
 #pragma unroll

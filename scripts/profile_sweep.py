@@ -20,15 +20,19 @@ def main():
     ap.add_argument("--chi", type=int, default=64)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default="0,1,2,4,3,5,6,7")
+    ap.add_argument("--pt-modes", default="0", help="PQD_PT_MODE values to cross with the ablations")
     args = ap.parse_args()
     import bench
     from pyaceqd_amd import engine
     sysd, grid, pt, rho0, ops, tr = bench.build_workload(args.traj, args.n_tau, args.chi)
     plans = {}
-    for v in [int(x) for x in args.variants.split(",")]:
-        os.environ["PQD_ABLATE"] = str(v)
-        plans[v] = engine.Plan(sysd, grid, rho0, ops, tr, pt=pt)
+    for pm in [int(x) for x in args.pt_modes.split(",")]:
+        for ab in [int(x) for x in args.variants.split(",")]:
+            os.environ["PQD_ABLATE"] = str(ab)
+            os.environ["PQD_PT_MODE"] = str(pm)
+            plans[f"pt{pm}/ab{ab}"] = engine.Plan(sysd, grid, rho0, ops, tr, pt=pt)
     os.environ.pop("PQD_ABLATE", None)
+    os.environ.pop("PQD_PT_MODE", None)
     res = {v: [] for v in plans}
     for v, p in plans.items():
         p.execute()
@@ -47,7 +51,7 @@ def main():
         ms = min(ws)
         out[v] = {"ms": ms, "us_per_step": 1e3 * ms / grid.n_steps,
                   "tflops_equiv": executed * F / (ms * 1e-3) / 1e12}
-        print(f"ablate={v}: sweep {ms:9.3f} ms  {1e3 * ms / grid.n_steps:7.3f} us/step  "
+        print(f"{v}: sweep {ms:9.3f} ms  {1e3 * ms / grid.n_steps:7.3f} us/step  "
               f"{out[v]['tflops_equiv']:6.2f} TF/s(full-work equiv)", flush=True)
     print(json.dumps({"traj": args.traj, "n_tau": args.n_tau, "chi": args.chi, "steps": grid.n_steps, "res": out}))
 

@@ -333,3 +333,21 @@ def test_bench_workload_small_vs_oracle():
     got = plan.download()
     ref = oracle.propagate(systems, grid, rho0, ops, tr, pt=pt, nthreads=8)
     cmp_lists(got, ref, 1e-11)
+
+
+@pytest.mark.parametrize("pt_mode", [0, 1, 2])
+@pytest.mark.parametrize("bt", [4, 8])
+@pytest.mark.parametrize("N,chi", [(2, 16), (3, 32), (4, 64), (5, 64), (6, 32)])
+def test_sweep_pt_contraction_modes(monkeypatch, pt_mode, bt, N, chi):
+    """PT contraction on the VALU (0), on the matrix cores (1, v_mfma_f64_4x4x4_4b) and mixed per wave (2)"""
+    if bt == 8 and N > 4:
+        pytest.skip("B=8 workgroups are built for N^2 <= 16")
+    monkeypatch.setenv("PQD_BT", str(bt))
+    monkeypatch.setenv("PQD_PT_MODE", str(pt_mode))
+    sysd, grid = H.random_system(N, n_steps=18, seed=7 * N + chi)
+    pt = ptmod.random_pt(N, chi, D=min(N * N, 8), n_slices=6, seed=chi + N, eps=0.15)
+    tr = _traj(grid.n_steps, N, 21, seed=2 * N + chi)
+    ops = [H.ketbra(N, 0, 0), H.ketbra(N, N - 1, 0), np.eye(N)]
+    rho0 = H.random_rho(N)
+    cmp_lists(engine.propagate(sysd, grid, rho0, ops, tr, pt=pt),
+              oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
