@@ -83,6 +83,20 @@ def bytes_per_launch(n_steps, n_init, chi, N=4, n_out=2, n_traj=1, D=16, execute
     return slices * D * chi * chi * 16 + 2 * n_steps * (N * N) ** 2 * 16 + n_out * 16 * executed_steps
 
 
+def pmc_traffic(cfg):
+    """HBM bytes per sweep launch from the committed PMC passes (profiles/pmc_traffic.json: FETCH_SIZE x2 +
+    WRITE_SIZE, gfx950-corrected) when they were measured on this exact workload; None otherwise"""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if any(rec.get("config", {}).get(k) != v for k, v in cfg.items()):
+        return None, None
+    return float(rec["hbm_bytes_per_launch"]), "profiles/pmc_traffic.json (" + rec.get("passes", "") + ")"
+
+
 def cpu_baseline(chi, target_s=15.0):
     """oracle/liboracle.so (plain-C port, OpenMP over trajectories) on a bounded sample of the same workload"""
     from oracle import oracle
@@ -179,6 +193,8 @@ def main():
     value = useful * args.steps * world / el
     F = flops_per_traj_step(4, args.chi, len(ops))
     achieved_tf = executed * F / (ms_sweep * 1e-3) / 1e12
+    traffic, traffic_src = pmc_traffic({"n_tau": args.n_tau, "traj_per_gpu": n_traj, "chi": args.chi,
+                                        "scan_points_per_gpu": args.scan, "t1_points": args.t1})
     line = {
         "metric": "propagation steps/sec (whole node), 4-level biexciton PT bond-dim 64",
         "value": value,
@@ -199,7 +215,8 @@ def main():
                    "useful_traj_steps_per_gpu": useful, "executed_traj_steps_per_gpu": executed,
                    "parallelism": f"scan{world}", "kernel_ms": {"pt_sweep": ms_sweep, "free_prop": ms_free}},
         "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved_tf / PEAK_FP64_TFLOPS, "traffic": None,
+                     "frac": achieved_tf / PEAK_FP64_TFLOPS, "traffic": traffic,
+                     "traffic_unit": "HBM bytes per launch", "traffic_source": traffic_src,
                      "kernel": "pt_sweep_kernel<16,64>",
                      "algorithmic": f"{F} flop/traj-step x {executed} executed traj-steps per launch",
                      "hbm_algorithmic_GBs": bytes_per_launch(grid.n_steps, 410, args.chi, n_traj=n_traj,
