@@ -70,10 +70,12 @@ def build_workload(n_t1, n_tau, chi, scan=1, scan_offset=0, dt=0.1, seed=1234):
     return (systems if scan > 1 else systems[0]), grid, pt, rho0, ops, tr
 
 
-def flops_per_traj_step(N=4, chi=64, n_out=2):
-    """F = 8 (D chi^2 + 2 chi N^4 + n_out N^2), D = N^2 PT rows contracted per step"""
+def flops_per_traj_step(N=4, chi=64, n_out=2, fused=True):
+    """F = 8 (D chi^2 + 2 chi N^4 + n_out N^2), D = N^2 PT rows contracted per step. The sweep
+    fuses M_b(n-1) and M_a(n) into one N^2 x N^2 operator on steps without MTOs, so the
+    executed algorithm does one column product per step: F_fused = 8 (D chi^2 + chi N^4 + n_out N^2)."""
     D = N * N
-    return 8 * (D * chi * chi + 2 * chi * N ** 4 + n_out * N * N)
+    return 8 * (D * chi * chi + (1 if fused else 2) * chi * N ** 4 + n_out * N * N)
 
 
 def bytes_per_launch(n_steps, n_init, chi, N=4, n_out=2, n_traj=1, D=16, executed_steps=0):
@@ -191,7 +193,8 @@ def main():
     useful = n_traj * args.n_tau
     executed = int(np.sum(tr.out_end + 1))
     value = useful * args.steps * world / el
-    F = flops_per_traj_step(4, args.chi, len(ops))
+    fused = os.environ.get("PQD_FUSE", "1") != "0"
+    F = flops_per_traj_step(4, args.chi, len(ops), fused=fused)
     achieved_tf = executed * F / (ms_sweep * 1e-3) / 1e12
     traffic, traffic_src = pmc_traffic({"n_tau": args.n_tau, "traj_per_gpu": n_traj, "chi": args.chi,
                                         "scan_points_per_gpu": args.scan, "t1_points": args.t1})
@@ -218,7 +221,8 @@ def main():
                      "frac": achieved_tf / PEAK_FP64_TFLOPS, "traffic": traffic,
                      "traffic_unit": "HBM bytes per launch", "traffic_source": traffic_src,
                      "kernel": "pt_sweep_kernel<16,64>",
-                     "algorithmic": f"{F} flop/traj-step x {executed} executed traj-steps per launch",
+                     "algorithmic": f"{F} flop/traj-step ({'fused' if fused else 'unfused'} half steps) x {executed} "
+                                    f"executed traj-steps per launch",
                      "hbm_algorithmic_GBs": bytes_per_launch(grid.n_steps, 410, args.chi, n_traj=n_traj,
                                                              executed_steps=executed) / (ms_sweep * 1e-3) / 1e9},
     }

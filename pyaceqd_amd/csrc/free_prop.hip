@@ -142,7 +142,56 @@ hipError_t launch_fp(const FreePropParams& p, hipStream_t s) {
     return hipGetLastError();
 }
 
+// Fused free half steps of consecutive PT steps. Between PT(m-1) and PT(m) a trajectory without MTOs at
+// step m applies M_b(m-1), reads its outputs, then applies M_a(m): one N2 x N2 operator F(m) = M_a(m) M_b(m-1)
+// does the same work with half the column-phase flops, and the outputs at step m are read from the state
+// before M_b(m-1) through W(m)[k] = ovec[k] . M_b(m-1) (a row vector per output operator).
+template <int N2>
+__global__ __launch_bounds__(256) void fuse_steps_kernel(FuseParams p) {
+    const int si = blockIdx.x / p.n_steps, m = blockIdx.x - si * p.n_steps + 1;  // m = 1..n_steps
+    const int tid = threadIdx.x;
+    const double2* Mb = p.M + ((size_t)si * 2 * p.n_steps + 2 * (m - 1) + 1) * N2 * N2;
+    if (m < p.n_steps) {
+        const double2* Ma = p.M + ((size_t)si * 2 * p.n_steps + 2 * m) * N2 * N2;
+        double2* F = p.F + ((size_t)si * p.n_steps + m) * N2 * N2;
+        for (int e = tid; e < N2 * N2; e += 256) {
+            const int r = e / N2, c = e - (e / N2) * N2;
+            double2 acc = c_zero();
+#pragma unroll
+            for (int k = 0; k < N2; ++k) c_fma(acc, Ma[r * N2 + k], Mb[k * N2 + c]);
+            F[e] = acc;
+        }
+    }
+    double2* W = p.W + ((size_t)si * (p.n_steps + 1) + m) * p.n_out * N2;
+    for (int e = tid; e < p.n_out * N2; e += 256) {
+        const int k = e / N2, a = e - (e / N2) * N2;
+        double2 acc = c_zero();
+#pragma unroll
+        for (int b = 0; b < N2; ++b) c_fma(acc, p.ovec[k * N2 + b], Mb[b * N2 + a]);
+        W[e] = acc;
+    }
+}
+
+template <int N2>
+hipError_t launch_fs(const FuseParams& p, hipStream_t s) {
+    const int nblk = p.n_sys * p.n_steps;
+    if (nblk <= 0) return hipSuccess;
+    hipLaunchKernelGGL(fuse_steps_kernel<N2>, dim3(nblk), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
 }  // namespace
+
+hipError_t launch_fuse_steps(int N2, const FuseParams& p, hipStream_t s) {
+    switch (N2) {
+        case 4: return launch_fs<4>(p, s);
+        case 9: return launch_fs<9>(p, s);
+        case 16: return launch_fs<16>(p, s);
+        case 25: return launch_fs<25>(p, s);
+        case 36: return launch_fs<36>(p, s);
+        default: return hipErrorInvalidValue;
+    }
+}
 
 hipError_t launch_free_prop(int N2, const FreePropParams& p, hipStream_t s) {
     switch (N2) {

@@ -71,6 +71,10 @@ struct SweepParams {
     const int4* ev;          // (step, after?1:0, superop index, 0), sorted per trajectory
     const double2* sop;      // MTO superoperators N2*N2 each
     double2* out;
+    const double2* F;        // fused half steps F(m) = M_a(m) M_b(m-1)   [n_sys][n_steps][N2 x N2]
+    const double2* W;        // output rows through M_b(m-1): W(m) = ovec . M_b(m-1)   [n_sys][n_steps+1][n_out][N2]
+    long long f_stride, w_stride;
+    int fuse;                // 1: steps without MTOs apply F(m) once instead of M_b(m-1) then M_a(m)
     int pt_mode;             // PT contraction: 0 VALU, 1 matrix cores (4x4x4_4b), 2 mixed per wave
     int ablate;              // diagnostics only (PQD_ABLATE): 1 skip PT, 2 skip column phases, 4 skip outputs
 };
@@ -108,7 +112,16 @@ struct FourTimeParams {
 };
 
 // launchers (defined in the .hip translation units)
+struct FuseParams {          // F(m) = M_a(m) M_b(m-1) (1 <= m < n_steps), W(m) = ovec . M_b(m-1) (1 <= m <= n_steps)
+    const double2* M;
+    double2* F;
+    double2* W;
+    const double2* ovec;
+    int n_sys, n_steps, n_out;
+};
+
 hipError_t launch_free_prop(int N2, const FreePropParams& p, hipStream_t s);
+hipError_t launch_fuse_steps(int N2, const FuseParams& p, hipStream_t s);
 hipError_t launch_sweep(int N2, int CHI, int BT, int n_blocks, const SweepParams& p, hipStream_t s);
 int sweep_max_bt(int N2);
 hipError_t launch_sweep_nopt(int N2, int n_blocks, const SweepParams& p, hipStream_t s);

@@ -202,8 +202,9 @@ struct pqd_plan {
     pqd_ctx* ctx = nullptr;
     int N2 = 0, CHI = 1, BT = 4, n_traj = 0, n_blocks = 0, n_steps = 0, n_sys = 1;
     bool nopt = true;
-    DevBuf<double2> L0, S, T, samples, M, rho0, ovec, sop, out;
+    DevBuf<double2> L0, S, T, samples, M, F, W, rho0, ovec, sop, out;
     DevBuf<FreePropSys> systab;
+    FuseParams fu{};
     DevBuf<int> sched, blk_traj, blk_end, blk_sys, traj_sys, wbeg, wend, ev_start;
     DevBuf<long long> woff;
     DevBuf<int4> ev;
@@ -526,6 +527,15 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     sp.traj_sys = P->traj_sys.p; sp.m_stride = (long long)2 * ns * m2; sp.wbeg = P->wbeg.p; sp.wend = P->wend.p;
     { const char* ab = getenv("PQD_ABLATE"); sp.ablate = ab ? atoi(ab) : 0; }
     { const char* pm = getenv("PQD_PT_MODE"); sp.pt_mode = pm ? atoi(pm) : 1; }
+    { const char* fz = getenv("PQD_FUSE"); sp.fuse = (!P->nopt && ns > 0 && (fz ? atoi(fz) : 1)) ? 1 : 0; }
+    if (sp.fuse) {
+        HIPCHK(P->F.alloc((size_t)n_sys * ns * m2));
+        HIPCHK(P->W.alloc((size_t)n_sys * (ns + 1) * n_out * N2));
+        P->fu = FuseParams{P->M.p, P->F.p, P->W.p, P->ovec.p, n_sys, ns, n_out};
+        sp.f_stride = (long long)ns * m2;
+        sp.w_stride = (long long)(ns + 1) * n_out * N2;
+    }
+    sp.F = P->F.p; sp.W = P->W.p;
     sp.woff = P->woff.p; sp.ev_start = P->ev_start.p; sp.ev = P->ev.p; sp.sop = P->sop.p; sp.out = P->out.p;
     HIPCHK(hipStreamSynchronize(s));
     *out = guard.release();
@@ -545,7 +555,10 @@ int pqd_plan_execute(pqd_plan* P, int32_t rebuild_free) {
     hipEvent_t e[3];
     for (int i = 0; i < 3; ++i) HIPCHK(hipEventCreate(&e[i]));
     HIPCHK(hipEventRecord(e[0], s));
-    if (rebuild_free && P->n_steps > 0) HIPCHK(launch_free_prop(P->N2, P->fp, s));
+    if (rebuild_free && P->n_steps > 0) {
+        HIPCHK(launch_free_prop(P->N2, P->fp, s));
+        if (P->sp.fuse) HIPCHK(launch_fuse_steps(P->N2, P->fu, s));
+    }
     HIPCHK(hipEventRecord(e[1], s));
     if (P->nopt)
         HIPCHK(launch_sweep_nopt(P->N2, P->n_traj, P->sp, s));

@@ -146,16 +146,60 @@ __device__ __forceinline__ void pt_row_mfma(const double2* __restrict__ Qg, doub
         for (int g = 0; g < NG; ++g) wr[(4 * rb + kk) * TS + 16 * g] = make_double2(cr[rb][g], ci[rb][g]);
 }
 
+// PT contraction of row alpha for BT = 8 on v_mfma_f64_16x16x4_f64 ("split complex"): the 16 MFMA rows are
+// [Re X; Im X] of the 8 trajectories, so two real GEMMs P1 = [Xr; Xi] Qr and P2 = [Xr; Xi] Qi hold all four
+// partial products: Cr = P1[top] - P2[bottom], Ci = P2[top] + P1[bottom]. C fragment rows (l>>4) + 4 r put
+// row b (r = 0, 1) and row b + 8 (r + 2) in the same lane, so the recombination is lane-local. Same operand
+// traffic as the 4x4x4 path, but the 16x16x4 instruction runs at the FP64 matrix peak and co-issues with VALU.
+template <int CHI, int RS, int TS>
+__device__ __forceinline__ void pt_row_mfma16(const double2* __restrict__ Qg, double2* st, int a, int lane) {
+    constexpr int NTL = CHI / 16, KSN = CHI / 4;
+    const int li = lane & 15, lk = lane >> 4;
+    const bool imag_row = (li & 8) != 0;
+    dbl4 p1[NTL], p2[NTL];
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) { p1[t] = dbl4{0, 0, 0, 0}; p2[t] = dbl4{0, 0, 0, 0}; }
+    const double2* xr = st + (li & 7) * TS + a * RS + lk;  // + 4 ks
+    const double2* qp = Qg + (size_t)lk * CHI + li;         // + 4 ks * CHI + 16 t
+    double2 qn[NTL];
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) qn[t] = qp[16 * t];
+#pragma unroll 2
+    for (int ks = 0; ks < KSN; ++ks) {
+        double2 qv[NTL];
+#pragma unroll
+        for (int t = 0; t < NTL; ++t) qv[t] = qn[t];
+        if (ks + 1 < KSN) {
+#pragma unroll
+            for (int t = 0; t < NTL; ++t) qn[t] = qp[(size_t)4 * (ks + 1) * CHI + 16 * t];
+        }
+        const double2 xv = xr[4 * ks];
+        const double av = imag_row ? xv.y : xv.x;
+#pragma unroll
+        for (int t = 0; t < NTL; ++t) {
+            p1[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, qv[t].x, p1[t], 0, 0, 0);
+            p2[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, qv[t].y, p2[t], 0, 0, 0);
+        }
+    }
+    double2* wr = st + a * RS + li;
+#pragma unroll
+    for (int t = 0; t < NTL; ++t)
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+            wr[(lk + 4 * r) * TS + 16 * t] = make_double2(p1[t][r] - p2[t][r + 2], p2[t][r] + p1[t][r + 2]);
+}
+
 template <int N2, int CHI, int BT>
 __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const double2* __restrict__ Mg,
-                                                           const double2* __restrict__ Qg0, double2* __restrict__ outg) {
+                                                           const double2* __restrict__ Qg0, double2* __restrict__ outg,
+                                                           const double2* __restrict__ Fg, const double2* __restrict__ Wg) {
     using L = SweepLayout<N2, CHI, BT>;
     constexpr int RS = L::RS, TS = L::TS, KD = L::KD, NCOL = L::NCOL;
     constexpr int NT = 64 * BT, NW = BT;  // threads, waves
     extern __shared__ __attribute__((aligned(16))) double2 smem[];
     double2* st = smem;
     double2* rbuf = smem + BT * TS;
-    __shared__ int s_traj[BT], s_wb[BT], s_we[BT];
+    __shared__ int s_traj[BT], s_wb[BT], s_we[BT], s_fz[BT];
     __shared__ long long s_wo[BT];
 
     const int tid = threadIdx.x;
@@ -168,10 +212,13 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
         s_wb[tid] = t >= 0 ? p.wbeg[t] : INT_MAX;
         s_we[tid] = t >= 0 ? p.wend[t] : -1;
         s_wo[tid] = t >= 0 ? p.woff[t] : 0;
+        s_fz[tid] = 0;
     }
     __syncthreads();
     const int n_end = p.blk_end[blockIdx.x];
     Mg += (size_t)p.blk_sys[blockIdx.x] * p.m_stride;
+    Fg += (size_t)p.blk_sys[blockIdx.x] * p.f_stride;
+    Wg += (size_t)p.blk_sys[blockIdx.x] * p.w_stride;
 
     // ---- initial augmented states rho0 (x) bond0 (thread -> column)
     for (int c = tid; c < NCOL; c += NT) {
@@ -197,6 +244,7 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
     __syncthreads();
 
     const int pj = lane & 15, pq = lane >> 4;
+    bool fz = false;  // this wave's trajectory sits between M_b(n-1) and M_a(n) unapplied (fused step n)
     for (int n = 0;; ++n) {
         // ------------------------------------------------------------ outputs at step n
         bool need = false;
@@ -224,7 +272,8 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
                 const int b = e / p.n_out, k = e - (e / p.n_out) * p.n_out;
                 if (s_wb[b] <= n && n <= s_we[b]) {
                     double2 s = c_zero();
-                    const double2* ov = p.ovec + (size_t)k * N2;
+                    // fused trajectories still hold the state before M_b(n-1): read it through W(n)
+                    const double2* ov = (s_fz[b] ? Wg + (size_t)n * p.n_out * N2 : p.ovec) + (size_t)k * N2;
                     for (int a = 0; a < N2; ++a) c_fma(s, ov[a], rbuf[b * N2 + a]);
                     outg[s_wo[b] + (long long)(n - s_wb[b]) * p.n_out + k] = s;
                 }
@@ -235,30 +284,43 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
         // ------------------------------------------------------------ column phase A
         const double2* Ma = Mg + (size_t)(2 * n) * N2 * N2;
         if (!(p.ablate & 2)) {
-            while (ev_cur < ev_lim) {  // applyBefore-false MTOs at step n
-                const int4 e = p.ev[ev_cur];
-                if (e.x != n || e.y != 1) break;
-                col_apply_mfma<N2, CHI, RS>(p.sop + (size_t)e.z * N2 * N2, stw, lane);
-                ++ev_cur;
+            if (fz) {  // no MTO at step n: M_b(n-1) and M_a(n) in one operator
+                col_apply_mfma<N2, CHI, RS>(Fg + (size_t)n * N2 * N2, stw, lane);
+            } else {
+                while (ev_cur < ev_lim) {  // applyBefore-false MTOs at step n
+                    const int4 e = p.ev[ev_cur];
+                    if (e.x != n || e.y != 1) break;
+                    col_apply_mfma<N2, CHI, RS>(p.sop + (size_t)e.z * N2 * N2, stw, lane);
+                    ++ev_cur;
+                }
+                col_apply_mfma<N2, CHI, RS>(Ma, stw, lane);
             }
-            col_apply_mfma<N2, CHI, RS>(Ma, stw, lane);
         }
         __syncthreads();
 
         // ------------------------------------------------------------ PT contraction
         if (!(p.ablate & 1)) {
             const double2* Qs = Qg0 + (size_t)p.sched[n] * p.D * CHI * CHI;
-            // pt_mode 0: VALU rows, 1: matrix-core rows, 2: mixed (waves 0..NW/2-1 start on the matrix cores,
+            // pt_mode 0: VALU rows, 1: matrix-core rows (4x4x4_4b), 3: split-complex 16x16x4 rows (BT = 8), 2: mixed (waves 0..NW/2-1 start on the matrix cores,
             // the others on the VALU, alternating per row), so the two FP64 pipes of a SIMD run concurrently
             int parity = (p.pt_mode == 2) ? ((wave >= NW / 2) ? 1 : 0) : 0;
             for (int a = wave; a < N2; a += NW) {
                 const double2* Qg = Qs + (size_t)p.gmap[a] * CHI * CHI;
                 const bool use_mfma = (p.pt_mode == 1) || (p.pt_mode == 2 && parity == 0);
                 parity ^= 1;
-                if (use_mfma) {
+                if constexpr (BT == 8) {
+                    if (p.pt_mode == 3) {
+                        pt_row_mfma16<CHI, RS, TS>(Qg, st, a, lane);
+                        continue;
+                    }
+                }
+                // the VALU rows are compiled for BT = 4 only: at BT = 8 their 128 accumulator VGPRs cap the
+                // whole kernel's allocation and spill, so BT = 8 runs modes 0/2 on the 4x4x4 path
+                if (BT == 8 || use_mfma || p.pt_mode == 3) {
                     pt_row_mfma<CHI, BT, RS, TS>(Qg, st, a, lane);
                     continue;
                 }
+                if constexpr (BT == 4) {
                 Qg += pj;
                 const double2* xr = st + a * RS + pq;
                 double2 acc[BT][KD];
@@ -321,13 +383,16 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
                         if (pq == 0) wr[b * TS] = h;
                     }
                 }
+                }  // VALU rows
             }
         }
         __syncthreads();
 
         // ------------------------------------------------------------ column phase B
         const double2* Mb = Ma + N2 * N2;
-        if (!(p.ablate & 2)) {
+        // fuse M_b(n) into the next step's operator unless this trajectory has an MTO at step n+1
+        fz = p.fuse && !(ev_cur < ev_lim && p.ev[ev_cur].x == n + 1);
+        if (!(p.ablate & 2) && !fz) {
             col_apply_mfma<N2, CHI, RS>(Mb, stw, lane);
             while (ev_cur < ev_lim) {  // applyBefore-true MTOs at step n+1
                 const int4 e = p.ev[ev_cur];
@@ -336,6 +401,7 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
                 ++ev_cur;
             }
         }
+        if (lane == 0) s_fz[wave] = fz ? 1 : 0;
         __syncthreads();
     }
 }
@@ -414,7 +480,8 @@ hipError_t launch_sw(int n_blocks, const SweepParams& p, hipStream_t s) {
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((pt_sweep_kernel<N2, CHI, BT>), dim3(n_blocks), dim3(64 * BT), L::LDS, s, p, p.M, p.Q, p.out);
+    hipLaunchKernelGGL((pt_sweep_kernel<N2, CHI, BT>), dim3(n_blocks), dim3(64 * BT), L::LDS, s, p, p.M, p.Q, p.out,
+                       p.F, p.W);
     return hipGetLastError();
 }
 

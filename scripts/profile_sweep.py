@@ -20,19 +20,22 @@ def main():
     ap.add_argument("--chi", type=int, default=64)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default="0,1,2,4,3,5,6,7")
-    ap.add_argument("--pt-modes", default="0", help="PQD_PT_MODE values to cross with the ablations")
+    ap.add_argument("--pt-modes", default="1", help="PQD_PT_MODE values to cross with the ablations")
+    ap.add_argument("--fuse-modes", default="1", help="PQD_FUSE values to cross with the ablations")
     args = ap.parse_args()
     import bench
     from pyaceqd_amd import engine
     sysd, grid, pt, rho0, ops, tr = bench.build_workload(args.traj, args.n_tau, args.chi)
     plans = {}
-    for pm in [int(x) for x in args.pt_modes.split(",")]:
-        for ab in [int(x) for x in args.variants.split(",")]:
-            os.environ["PQD_ABLATE"] = str(ab)
-            os.environ["PQD_PT_MODE"] = str(pm)
-            plans[f"pt{pm}/ab{ab}"] = engine.Plan(sysd, grid, rho0, ops, tr, pt=pt)
-    os.environ.pop("PQD_ABLATE", None)
-    os.environ.pop("PQD_PT_MODE", None)
+    for fm in [int(x) for x in args.fuse_modes.split(",")]:
+        for pm in [int(x) for x in args.pt_modes.split(",")]:
+            for ab in [int(x) for x in args.variants.split(",")]:
+                os.environ["PQD_ABLATE"] = str(ab)
+                os.environ["PQD_PT_MODE"] = str(pm)
+                os.environ["PQD_FUSE"] = str(fm)
+                plans[f"fuse{fm}/pt{pm}/ab{ab}"] = engine.Plan(sysd, grid, rho0, ops, tr, pt=pt)
+    for k in ("PQD_ABLATE", "PQD_PT_MODE", "PQD_FUSE"):
+        os.environ.pop(k, None)
     res = {v: [] for v in plans}
     for v, p in plans.items():
         p.execute()
@@ -45,7 +48,7 @@ def main():
             f, w, n = p.timing(reset=True)
             res[v].append(w)
     executed = int(sum(tr.out_end + 1))
-    F = bench.flops_per_traj_step(4, args.chi, len(ops))
+    F = bench.flops_per_traj_step(4, args.chi, len(ops), fused=False)  # full-work equivalent (unfused)
     out = {}
     for v, ws in res.items():
         ms = min(ws)

@@ -324,8 +324,11 @@ def test_multi_system_scan(with_pt):
               oracle.propagate(systems, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
 
 
-def test_bench_workload_small_vs_oracle():
-    """the bench workload itself (scan of G2 sweeps, chi=64, B=8 path) at reduced n_tau vs the oracle"""
+@pytest.mark.parametrize("fuse", ["0", "1"])
+def test_bench_workload_small_vs_oracle(monkeypatch, fuse):
+    """the bench workload itself (scan of G2 sweeps, chi=64, B=8 path) at reduced n_tau vs the oracle,
+    with the fused half steps (default) and without"""
+    monkeypatch.setenv("PQD_FUSE", fuse)
     import bench
     systems, grid, pt, rho0, ops, tr = bench.build_workload(16, 60, 64, scan=2)
     plan = engine.Plan(systems, grid, rho0, ops, tr, pt=pt)
@@ -335,15 +338,18 @@ def test_bench_workload_small_vs_oracle():
     cmp_lists(got, ref, 1e-11)
 
 
-@pytest.mark.parametrize("pt_mode", [0, 1, 2])
+@pytest.mark.parametrize("pt_mode", [0, 1, 2, 3])
 @pytest.mark.parametrize("bt", [4, 8])
 @pytest.mark.parametrize("N,chi", [(2, 16), (3, 32), (4, 64), (5, 64), (6, 32)])
-def test_sweep_pt_contraction_modes(monkeypatch, pt_mode, bt, N, chi):
-    """PT contraction on the VALU (0), on the matrix cores (1, v_mfma_f64_4x4x4_4b) and mixed per wave (2)"""
+@pytest.mark.parametrize("fuse", ["0", "1"])
+def test_sweep_pt_contraction_modes(monkeypatch, pt_mode, bt, N, chi, fuse):
+    """PT contraction on the VALU (0), on the matrix cores (1, v_mfma_f64_4x4x4_4b; 3, split-complex
+    v_mfma_f64_16x16x4 at B = 8) and mixed per wave (2)"""
     if bt == 8 and N > 4:
         pytest.skip("B=8 workgroups are built for N^2 <= 16")
     monkeypatch.setenv("PQD_BT", str(bt))
     monkeypatch.setenv("PQD_PT_MODE", str(pt_mode))
+    monkeypatch.setenv("PQD_FUSE", fuse)
     sysd, grid = H.random_system(N, n_steps=18, seed=7 * N + chi)
     pt = ptmod.random_pt(N, chi, D=min(N * N, 8), n_slices=6, seed=chi + N, eps=0.15)
     tr = _traj(grid.n_steps, N, 21, seed=2 * N + chi)
