@@ -18,7 +18,8 @@ choice is a documented switch):
     user pulse files (`pulse_file_x/_y`, "t Re Im") are linearly interpolated and held at both ends;
   * MTO at time T acts at step round((T - t_start)/dt): applyBefore "true" before that step's
     output, otherwise after it; "" -> A rho A^dag, "_left" -> A rho, "_right" -> rho A;
-  * phonons: PT from `pt_file` (pqd .npz, pyaceqd_amd.pt) or a ProcessTensor object.
+  * phonons: PT from `pt_file` (pqd .npz, pyaceqd_amd.pt) or a ProcessTensor object; when no PT file exists the
+    Gaussian-bath PT is generated from the same parameters as ACE's generate file (pyaceqd_amd.ptgen) and cached.
 """
 import os
 
@@ -110,16 +111,48 @@ def _rf_pulses(pulses):
     return new
 
 
-def _resolve_pt(pt_file, dim):
+def _resolve_pt(pt_file, boson_mat, *, dt, t_mem, ae, temperature, threshold, factor_ah, boson_e_max, J_file,
+                J_to_file, use_infinite, system_prefix, temp_dir, verbose):
+    """The PT for phonons=True (general_system.py:146-211): a ProcessTensor object is used as is; an existing pqd
+    PT container (`<pt_file>.npz`, or `pt_file` itself if it is one) is loaded; otherwise the Gaussian-bath PT is
+    generated from the same parameters ACE's generate file holds (pyaceqd_amd.ptgen) and cached under the
+    reference's file name (plus `.npz`) so later calls reuse it, as the reference does with its `_initial` files."""
     if isinstance(pt_file, ProcessTensor):
         return pt_file
-    from ..pt import load_pt
-    if pt_file is None or not os.path.exists(str(pt_file)):
-        raise NotImplementedError(
-            "phonons=True needs a process tensor: pass pt_file=<pqd .npz PT> (pyaceqd_amd.pt.save_pt) or a "
-            "ProcessTensor. Generating a Gaussian-bath PT (ACE dont_propagate/write_PT) is not implemented yet "
-            f"(requested {pt_file!r}).")
-    return load_pt(str(pt_file))
+    from ..pt import load_pt, save_pt
+    from .. import ptgen
+    if pt_file is None:
+        pt_file = ptgen.pt_cache_name(system_prefix, ae, temperature, threshold, t_mem, dt, J_file=J_file,
+                                      use_infinite=use_infinite)
+        pt_file = os.path.join(temp_dir, pt_file) if temp_dir else pt_file
+    pt_file = str(pt_file)
+    for cand in (pt_file, pt_file + ".npz"):
+        if os.path.isfile(cand) and J_to_file is None:
+            if verbose:
+                print("using pt_file " + cand)
+            return load_pt(cand)
+    thr = float(threshold) if "e" in str(threshold).lower() or float(threshold) < 1 else 10.0 ** (-float(threshold))
+    if verbose:
+        print("{} not found. Calculating...".format(pt_file))
+    pt = ptgen.qd_phonon_pt(boson_mat, dt, t_mem=t_mem, ae=ae, temperature=temperature, threshold=thr,
+                            factor_ah=factor_ah, boson_e_max=boson_e_max, J_file=J_file, use_infinite=use_infinite,
+                            verbose=verbose)
+    try:
+        save_pt(pt_file + ".npz", pt, dim=boson_mat.shape[0])
+    except OSError:
+        pass
+    return pt
+
+
+def _write_J(J_to_file, ae, factor_ah, J_file):
+    """`Boson_J_print <file> 0 15 2000` (general_system.py:186-187, 203-209)."""
+    from .. import ptgen
+    if J_file is not None:
+        J = ptgen.J_from_file(J_file)
+    else:
+        ah = None if factor_ah is None else ae / factor_ah
+        J = lambda w: ptgen.qd_phonon_J(w, ae=ae, ah=ah)  # noqa: E731
+    ptgen.write_J(J_to_file, J, 0.0, 15.0, 2000)
 
 
 def system_ace_stream(t_start, t_end, *pulses, dt=0.01, phonons=False, t_mem=20.48, ae=3.0, temperature=1,
@@ -144,6 +177,8 @@ def system_ace_stream(t_start, t_end, *pulses, dt=0.01, phonons=False, t_mem=20.
             multitime_op = [multitime_op]
         for m in multitime_op:
             check_multitime(m, verbose)
+    if phonons and J_to_file:
+        _write_J(J_to_file, ae, factor_ah, J_file)
     if prepare_only:
         return [np.array([0, 0]) for _ in range(1 + len(output_ops))]
     if dressedstates or print_H:
@@ -240,7 +275,12 @@ def system_ace_stream(t_start, t_end, *pulses, dt=0.01, phonons=False, t_mem=20.
         return M[1] @ M[0]
 
     # ---------------------------------------------------------------- environment
-    pt = _resolve_pt(pt_file, dim) if phonons else None
+    pt = None
+    if phonons:
+        pt = _resolve_pt(pt_file, mat(boson_op), dt=dt, t_mem=t_mem, ae=ae, temperature=temperature,
+                         threshold=threshold, factor_ah=factor_ah, boson_e_max=boson_e_max, J_file=J_file,
+                         J_to_file=J_to_file, use_infinite=use_infinite, system_prefix=system_prefix,
+                         temp_dir=temp_dir, verbose=verbose)
 
     # ---------------------------------------------------------------- trajectories
     out_mats = [mat(s) for s in output_ops]

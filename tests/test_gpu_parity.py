@@ -357,3 +357,47 @@ def test_sweep_pt_contraction_modes(monkeypatch, pt_mode, bt, N, chi, fuse):
     rho0 = H.random_rho(N)
     cmp_lists(engine.propagate(sysd, grid, rho0, ops, tr, pt=pt),
               oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
+
+
+# --------------------------------------------------------------------------------- generated phonon PTs
+def test_tls_phonons_generated_pt_vs_oracle(monkeypatch, tmp_path):
+    """config C2 shape: tls with a generated QD-phonon PT (pyaceqd_amd.ptgen, bond capped at 32 by the threshold
+    choice / cap), driver path on the GPU vs the same lowering on the CPU oracle; phonons visibly damp the Rabi
+    rotation relative to the phonon-free run"""
+    from pyaceqd_amd.two_level_system.tls import tls
+    from pyaceqd_amd.pulses import ChirpedPulse
+    from pyaceqd_amd import ptgen, opgrammar
+    eta, delta = ptgen.eta_coefficients(lambda w: ptgen.qd_phonon_J(w, ae=3.0), 4.0, 0.1, 30)
+    pt = ptgen.build_gaussian_pt(opgrammar.to_matrix("1.000*|1><1|_2", 2), 0.1, eta, delta, threshold=1e-8,
+                                 max_bond=32)
+    assert pt.chi == 32
+    p = ChirpedPulse(tau_0=3, e_start=0, e0=5, t0=15)
+    kw = dict(dt=0.1, lindblad=True, phonons=True, pt_file=pt, temp_dir=str(tmp_path) + "/")
+    a = tls(0, 60, p, **kw)
+    free = tls(0, 60, p, dt=0.1, lindblad=True)
+    _oracle_patch(monkeypatch)
+    b = tls(0, 60, p, **kw)
+    assert rel(a, b) < 1e-11
+    assert np.max(np.abs(a[2] - free[2])) > 1e-2
+    # trace: exact without phonons; with the chi=32-capped PT it drifts at the truncation level (~1e-5)
+    assert np.max(np.abs(a[1] + a[2] - 1)) < 1e-4
+
+
+def test_biexciton_generated_pt_two_time_vs_oracle(monkeypatch, tmp_path):
+    """biexciton with a generated chi=64 phonon PT (explicit + repeated slices) through the batched G2 sweep"""
+    from pyaceqd_amd.four_level_system.linear import biexciton
+    from pyaceqd_amd.two_time.correlations import three_op_two_time
+    from pyaceqd_amd.pulses import ChirpedPulse
+    from pyaceqd_amd import ptgen, opgrammar
+    eta, delta = ptgen.eta_coefficients(lambda w: ptgen.qd_phonon_J(w, ae=3.0), 4.0, 0.1, 6)
+    pt = ptgen.build_gaussian_pt(opgrammar.to_matrix("1*(|1><1|_4 + |2><2|_4) + 2*|3><3|_4", 4), 0.1, eta, delta,
+                                 threshold=1e-10, max_bond=64)
+    assert pt.chi == 64 and pt.D == 9
+    p = ChirpedPulse(tau_0=3, e_start=-2.0, e0=1.0, t0=5)
+    t_axis = np.round(np.arange(8) * 0.5, 6)
+    kw = dict(opA="|3><1|_4", opB="|1><1|_4", opC="|1><3|_4", tau_max=6.0, dt=0.1)
+    opts = lambda: {"lindblad": True, "phonons": True, "pt_file": pt}  # noqa: E731
+    _, _, G = three_op_two_time(biexciton, t_axis, p, options=opts(), **kw)
+    _oracle_patch(monkeypatch)
+    _, _, Gr = three_op_two_time(biexciton, t_axis, p, options=opts(), **kw)
+    assert rel(G, Gr) < 1e-10

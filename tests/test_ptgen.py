@@ -1,0 +1,118 @@
+"""Gaussian-bath PT generator (pyaceqd_amd/ptgen.py; replaces ACE's `write_PT`, general_system.py:152-211).
+
+ACE is absent, so parity with ACE's PT files is unpinned. The generator is pinned by:
+  * the closed-form independent-boson coherence (the eta_k quadrature and sign/polaron-shift conventions);
+  * the exact uncompressed shift-register PT of oracle/ptgen_oracle.py with driving and Lindblad terms (the MPS
+    compression, the s+/s- split step, the trace-adapted basis and the stationary repeated slice).
+Propagation here runs through the C oracle (CPU); the GPU runs the same PTs in tests/test_gpu_parity.py.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle, ptgen_oracle
+from pyaceqd_amd import ptgen
+from pyaceqd_amd.constants import hbar
+from pyaceqd_amd.engine import Grid, System, Trajectories
+from tests import helpers as H
+
+QDJ = lambda w: ptgen.qd_phonon_J(w, ae=3.0)  # noqa: E731
+
+
+def test_qd_J_small_omega_and_units():
+    """J ~ w^3 (D_e - D_h)^2 / (4 pi^2 rho hbar c^5) for w -> 0, in 1/ps"""
+    w = np.array([1e-4, 2e-4])
+    pref = (ptgen.QD_DE - ptgen.QD_DH) ** 2 * 1.602176634e-19 ** 2 / (
+        4 * np.pi ** 2 * ptgen.QD_RHO * 1.054571817e-34 * ptgen.QD_CS ** 5) * 1e36 * 1e-12
+    assert np.allclose(QDJ(w) / w ** 3, pref, rtol=1e-6)
+    assert QDJ(np.array([0.0]))[0] == 0.0
+    # the Gaussian form factor cuts J off above ~ 2 c_s / a
+    assert QDJ(np.array([12.0]))[0] < 1e-3 * QDJ(np.array([2.0]))[0]
+
+
+def test_eta_reproduces_closed_form_ibm():
+    """sum of the discretised eta_k = the continuous double integral of C(t) (pure dephasing is exact at any dt)"""
+    dt, K, T = 0.1, 40, 4.0
+    eta, delta = ptgen.eta_coefficients(QDJ, T, dt, K)
+    disc = ptgen_oracle.ibm_coherence_discrete(eta, delta, dt, K)
+    exact = ptgen_oracle.ibm_coherence_exact(QDJ, T, dt * np.arange(K + 1))
+    assert np.max(np.abs(disc - exact)) < 1e-9
+    # the coherence drops to the Franck-Condon value |<B>|^2 and stays there; the polaron shift is removed
+    assert 0.3 < abs(disc[-1]) < 0.5 and abs(np.angle(disc[-1])) < 1e-3
+
+
+def test_polaron_shift_and_zero_temperature():
+    eta0, d0 = ptgen.eta_coefficients(QDJ, 0.0, 0.1, 5)
+    eta4, d4 = ptgen.eta_coefficients(QDJ, 4.0, 0.1, 5)
+    assert d0 == d4 > 0                                   # Delta = int J/w is temperature independent
+    assert np.allclose(eta0.imag, eta4.imag)              # the dissipative part does not depend on T
+    assert np.all(eta4[1:].real >= eta0[1:].real - 1e-15)
+
+
+@pytest.mark.parametrize("lam,K,n_init", [([0, 1], 3, 9), ([0, 1, 1], 2, 4), ([0, 1, 1, 2], 2, 7), ([0, 2], 1, 2)])
+def test_generator_matches_exact_shift_register(lam, K, n_init):
+    """driven, damped N-level system with a 30x enhanced bath: compressed generator (threshold 1e-14, explicit
+    slices then the repeated stationary slice) vs the exact shift-register PT over 40 steps"""
+    N = len(lam)
+    A = np.diag(np.array(lam, dtype=float))
+    J = lambda w: 30 * QDJ(w)  # noqa: E731
+    eta, delta = ptgen.eta_coefficients(J, 4.0, 0.1, K)
+    sysd, grid = H.random_system(N, n_steps=40, seed=3 + N)
+    rho0 = H.random_rho(N)
+    ops = [H.ketbra(N, i, j) for i in range(N) for j in range(N)]
+    tr = Trajectories(np.array([0, 5]), np.array([40, 33]))
+    pg = ptgen.build_gaussian_pt(A, 0.1, eta, delta, threshold=1e-14, max_bond=0, n_init=n_init)
+    pe = ptgen_oracle.exact_if_pt(A, eta, delta, 0.1)
+    assert pg.chi <= pe.chi
+    got = oracle.propagate(sysd, grid, rho0, ops, tr, pt=pg)
+    ref = oracle.propagate(sysd, grid, rho0, ops, tr, pt=pe)
+    bare = oracle.propagate(sysd, grid, rho0, ops, tr)
+    for a, b, c in zip(got, ref, bare):
+        assert np.max(np.abs(a - b)) < 1e-11
+        assert np.max(np.abs(b - c)) > 1e-2        # the bath matters at this coupling
+
+
+def test_generated_pt_ibm_long_run():
+    """QD phonons, K = 8, threshold 1e-8: coherence vs the discretised IBM solution for 8K steps (2K explicit
+    slices, then the repeated slice), trace preserved. The truncation error grows ~ threshold per step."""
+    dt, K = 0.1, 8
+    eta, delta = ptgen.eta_coefficients(QDJ, 4.0, dt, K)
+    pt = ptgen.build_gaussian_pt(np.diag([0.0, 1.0]), dt, eta, delta, threshold=1e-8, max_bond=0)
+    n = 8 * K
+    out = oracle.propagate(System(dim=2, H0=np.zeros((2, 2))), Grid(0.0, dt, n), 0.5 * np.ones((2, 2), complex),
+                           [H.ketbra(2, 0, 1), np.eye(2)], Trajectories(np.array([0]), np.array([n])), pt=pt)[0]
+    ex = ptgen_oracle.ibm_coherence_discrete(eta, delta, dt, n)
+    assert np.max(np.abs(out[:, 0] - ex)) < 1e-5
+    assert np.max(np.abs(out[:, 1] - 1)) < 1e-9
+
+
+def test_bond_cap_and_padding():
+    eta, delta = ptgen.eta_coefficients(QDJ, 4.0, 0.1, 8)
+    pt = ptgen.build_gaussian_pt(np.diag([0.0, 1.0]), 0.1, eta, delta, threshold=1e-12, max_bond=16)
+    assert pt.chi == 16 and pt.n_init == 16 and pt.n_slices == 17
+    assert pt.D == 4 and list(pt.gmap) == [0, 1, 2, 3]
+
+
+def test_driver_generates_and_caches_pt(tmp_path):
+    """system_ace_stream(phonons=True) without a PT file: generate from the ACE generate-file parameters, cache
+    under the reference's name (+ .npz), reuse on the next call; J_to_file writes J(omega)"""
+    from pyaceqd_amd.general_system import general_system as gs
+    from pyaceqd_amd import opgrammar
+    B = opgrammar.to_matrix("1.000*|1><1|_2", 2)
+    kw = dict(dt=0.1, t_mem=0.5, ae=3.0, temperature=4, threshold="9", factor_ah=None, boson_e_max=7, J_file=None,
+              J_to_file=None, use_infinite=True, system_prefix="tls", temp_dir=str(tmp_path) + os.sep, verbose=False)
+    pt = gs._resolve_pt(None, B, **kw)
+    name = str(tmp_path / ptgen.pt_cache_name("tls", 3.0, 4, "9", 0.5, 0.1, use_infinite=True)) + ".npz"
+    assert os.path.isfile(name)
+    pt2 = gs._resolve_pt(None, B, **kw)
+    assert np.array_equal(pt.Q, pt2.Q) and pt.n_init == 10
+    jf = str(tmp_path / "J.dat")
+    gs._write_J(jf, 3.0, None, None)
+    d = np.loadtxt(jf)
+    assert d.shape == (2000, 2) and abs(d[-1, 0] - 15 / hbar) < 1e-9
+    assert np.allclose(d[:, 1], QDJ(d[:, 0]))
+    # J_file round trip
+    J2 = ptgen.J_from_file(jf)
+    w = np.linspace(0.5, 5, 7)
+    assert np.allclose(J2(w), QDJ(w), rtol=2e-3)
