@@ -71,6 +71,7 @@ int pad_chi(int chi) {
     if (chi <= 16) return 16;
     if (chi <= 32) return 32;
     if (chi <= 64) return 64;
+    if (chi <= 128) return 128;
     return -1;
 }
 
@@ -301,7 +302,7 @@ int pqd_pt_create(pqd_ctx* ctx, int32_t dim, const pqd_pt_desc* d, pqd_pt** out)
     if (dim < 2 || dim > 6) return fail(PQD_ERR_UNSUPPORTED, "dim %d", dim);
     const int N2 = dim * dim;
     const int CHI = pad_chi(d->chi);
-    if (d->chi < 1 || CHI < 0) return fail(PQD_ERR_UNSUPPORTED, "chi %d not in [1, 64]", d->chi);
+    if (d->chi < 1 || CHI < 0) return fail(PQD_ERR_UNSUPPORTED, "chi %d not in [1, 128]", d->chi);
     if (d->D < 1 || d->n_slices < 1) return fail(PQD_ERR_ARG, "D and n_slices must be >= 1");
     if (!d->Q || !d->closure || !d->closure0 || !d->bond0 || !d->gmap) return fail(PQD_ERR_ARG, "NULL PT array");
     for (int a = 0; a < N2; ++a)
@@ -489,6 +490,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     }
     int BT = (sweep_max_bt(N2) >= 8 && tr->n_traj >= 8 * n_cu) ? 8 : 4;
     if (const char* e = getenv("PQD_BT")) BT = std::min(atoi(e) >= 8 ? 8 : 4, sweep_max_bt(N2));
+    if (P->CHI > 64) BT = 4;  // chi = 128: only four augmented states fit the LDS
     P->BT = BT;
     std::vector<int> bt, be, bs;
     for (size_t k = 0; k < order.size();) {  // blocks never mix systems

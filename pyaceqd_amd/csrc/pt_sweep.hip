@@ -314,13 +314,14 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
                         continue;
                     }
                 }
-                // the VALU rows are compiled for BT = 4 only: at BT = 8 their 128 accumulator VGPRs cap the
-                // whole kernel's allocation and spill, so BT = 8 runs modes 0/2 on the 4x4x4 path
-                if (BT == 8 || use_mfma || p.pt_mode == 3) {
+                // the VALU rows are compiled for BT = 4 and chi <= 64 only: at BT = 8 (or chi = 128) their
+                // accumulators cap the whole kernel's VGPR allocation and spill, so those run modes 0/2 on the
+                // 4x4x4 path
+                if (BT == 8 || CHI > 64 || use_mfma || p.pt_mode == 3) {
                     pt_row_mfma<CHI, BT, RS, TS>(Qg, st, a, lane);
                     continue;
                 }
-                if constexpr (BT == 4) {
+                if constexpr (BT == 4 && CHI <= 64) {
                 Qg += pj;
                 const double2* xr = st + a * RS + pq;
                 double2 acc[BT][KD];
@@ -491,6 +492,10 @@ hipError_t launch_sw_chi(int CHI, int n_blocks, const SweepParams& p, hipStream_
         case 16: return launch_sw<N2, 16, BT>(n_blocks, p, s);
         case 32: return launch_sw<N2, 32, BT>(n_blocks, p, s);
         case 64: return launch_sw<N2, 64, BT>(n_blocks, p, s);
+        case 128:
+            // chi = 128 keeps 4 augmented states of N2 <= 16 in LDS (132 KiB); larger N2 or BT do not fit
+            if constexpr (BT == 4 && N2 <= 16) return launch_sw<N2, 128, BT>(n_blocks, p, s);
+            return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
     }
 }
@@ -499,7 +504,7 @@ hipError_t launch_sw_chi(int CHI, int n_blocks, const SweepParams& p, hipStream_
 
 bool sweep_supported(int N2, int CHI) {
     return (N2 == 4 || N2 == 9 || N2 == 16 || N2 == 25 || N2 == 36) &&
-           (CHI == 1 || CHI == 16 || CHI == 32 || CHI == 64);
+           (CHI == 1 || CHI == 16 || CHI == 32 || CHI == 64 || (CHI == 128 && N2 <= 16));
 }
 
 // trajectories per workgroup that fit the LDS for this N2 (8 halves the per-trajectory PT-slice traffic)

@@ -210,7 +210,7 @@ class GaussianPTBuilder:
     instead of n_lambda^2 blocks: (n_lambda c)^3 instead of (n_lambda^2 c)^3 per site."""
 
     def __init__(self, boson_op, eta, delta_pol=0.0, dt=None, threshold=1e-10, max_bond=64,
-                 subtract_polaron_shift=True, tail_threshold=None, tail_max_bond=None):
+                 subtract_polaron_shift=True, tail_threshold=None, tail_max_bond=None, trace_basis=True):
         self.gmap, self.pairs, self.xis = _coupling_structure(boson_op)
         self.eta = np.asarray(eta, dtype=np.complex128)
         self.K = len(self.eta) - 1
@@ -232,10 +232,13 @@ class GaussianPTBuilder:
         order = [x0] + [q for q in range(P) if q != x0]       # xi = 0 is basis element 0
         self.xis = self.xis[order]
         Bm = np.eye(P, dtype=np.complex128)
-        Bm[1:, 0] = -1.0
         Binv = np.eye(P, dtype=np.complex128)
-        Binv[1:, 0] = 1.0
+        if trace_basis:
+            Bm[1:, 0] = -1.0
+            Binv[1:, 0] = 1.0
         self.B, self.Binv = Bm, Binv
+        self.one = Bm @ np.ones(P, dtype=np.complex128)         # the constant function (no past) in this basis
+        self.cvec = Binv[0]                                      # f(0) = cvec . g: the trace closure
         xi_of = np.array([[int(np.argmin(np.abs(self.xis - (a - b)))) for b in lams] for a in lams])  # [ip, im]
         self.reindex = Binv[xi_of]                               # (ip, im, P): f(lam_ip - lam_im) = . g
         sp = np.array([p[0] for p in self.pairs])
@@ -250,18 +253,16 @@ class GaussianPTBuilder:
         self.Fp = np.einsum("pq,akq,qr->akpr", Bm, dplus, Binv, optimize=True)                   # (nl, K, P, P)
         self.Fm = np.einsum("pq,akq,qr->akpr", Bm, dminus, Binv, optimize=True)
         self.newp = np.einsum("pq,aq->ap", Bm, dplus[:, -1, :]) if self.K else None              # (nl, P)
-        one = np.zeros(P, dtype=np.complex128)
-        one[0] = 1.0
-        self.tail = [one.reshape(1, P, 1).copy() for _ in range(self.K)]
+        self.tail = [self.one.reshape(1, P, 1).copy() for _ in range(self.K)]
         self.r = 1
 
     def closure(self, tail=None):
         tail = self.tail if tail is None else tail
         if not tail:
             return np.ones(1, dtype=np.complex128)
-        v = tail[-1][:, 0, :]
+        v = np.einsum("p,lpr->lr", self.cvec, tail[-1])
         for T in reversed(tail[:-1]):
-            v = T[:, 0, :] @ v
+            v = np.einsum("p,lpr->lr", self.cvec, T) @ v
         return v[:, 0]
 
     def _advance(self, tail):
@@ -315,11 +316,11 @@ class GaussianPTBuilder:
 
 
 def build_gaussian_pt(boson_op, dt, eta, delta_pol=0.0, n_init=None, threshold=1e-10, max_bond=64, repeat=True,
-                      subtract_polaron_shift=True, verbose=False, tail_max_bond=None):
+                      subtract_polaron_shift=True, verbose=False, tail_max_bond=None, **builder_kw):
     """ProcessTensor with n_init explicit slices and (repeat=True) one stationary slice repeated forever.
     n_init defaults to 2 K (ACE: `te 2*t_mem`, general_system.py:160)."""
     b = GaussianPTBuilder(boson_op, eta, delta_pol, dt, threshold, max_bond, subtract_polaron_shift,
-                          tail_max_bond=tail_max_bond)
+                          tail_max_bond=tail_max_bond, **builder_kw)
     K = b.K
     n_init = 2 * max(K, 1) if n_init is None else int(n_init)
     Qs, cls = [], []
@@ -346,8 +347,11 @@ def build_gaussian_pt(boson_op, dt, eta, delta_pol=0.0, n_init=None, threshold=1
 
 
 def qd_phonon_pt(boson_op, dt, t_mem=20.48, ae=3.0, temperature=1.0, threshold=1e-10, factor_ah=None,
-                 boson_e_max=7.0, J_file=None, use_infinite=False, max_bond=64, n_init=None, verbose=False):
-    """The PT of general_system.py:152-211's generate file, from its own parameters."""
+                 boson_e_max=7.0, J_file=None, use_infinite=False, max_bond=None, n_init=None, verbose=False):
+    """The PT of general_system.py:152-211's generate file, from its own parameters. The bond is capped at what
+    the sweep kernel holds in LDS: 128 for N <= 4, 64 above."""
+    if max_bond is None:
+        max_bond = 128 if np.asarray(boson_op).shape[0] <= 4 else 64
     if J_file is not None:
         J = J_from_file(J_file)
     else:

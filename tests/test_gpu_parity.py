@@ -65,8 +65,10 @@ def test_sweep_no_pt(N, n_traj):
 
 
 @pytest.mark.parametrize("N", [2, 3, 4, 5, 6])
-@pytest.mark.parametrize("chi", [8, 16, 32, 64])
+@pytest.mark.parametrize("chi", [8, 16, 32, 64, 100, 128])
 def test_sweep_pt(N, chi):
+    if chi > 64 and N > 4:
+        pytest.skip("chi > 64 is built for N^2 <= 16 (LDS)")
     sysd, grid = H.random_system(N, n_steps=24, seed=3 * N + chi)
     pt = ptmod.random_pt(N, chi, D=min(N * N, 9), n_slices=7, seed=chi, eps=0.15)
     tr = _traj(grid.n_steps, N, 6, seed=N * chi)
@@ -103,6 +105,14 @@ def test_invalid_arguments_raise():
     with pytest.raises(ValueError, match="MTO"):
         engine.propagate(sysd, grid, H.ketbra(2, 0, 0), [np.eye(2)],
                          Trajectories(np.array([0]), np.array([5]), [MTO(0, 9, False, 1, np.eye(2))]))
+    from pyaceqd_amd import _lib
+    with pytest.raises(_lib.PQDError, match="chi 129"):
+        engine.propagate(sysd, grid, H.ketbra(2, 0, 0), [np.eye(2)], Trajectories(np.array([0]), np.array([5])),
+                         pt=ptmod.random_pt(2, 129, n_slices=2))
+    s6, g6 = H.random_system(6, n_steps=3, seed=0)
+    with pytest.raises(_lib.PQDError, match="CHI=128"):
+        engine.propagate(s6, g6, H.ketbra(6, 0, 0), [np.eye(6)], Trajectories(np.array([0]), np.array([3])),
+                         pt=ptmod.random_pt(6, 100, D=4, n_slices=2))
 
 
 # --------------------------------------------------------------------------------- full-size properties (C3)
@@ -340,13 +350,15 @@ def test_bench_workload_small_vs_oracle(monkeypatch, fuse):
 
 @pytest.mark.parametrize("pt_mode", [0, 1, 2, 3])
 @pytest.mark.parametrize("bt", [4, 8])
-@pytest.mark.parametrize("N,chi", [(2, 16), (3, 32), (4, 64), (5, 64), (6, 32)])
+@pytest.mark.parametrize("N,chi", [(2, 16), (3, 32), (4, 64), (5, 64), (6, 32), (2, 128), (4, 128)])
 @pytest.mark.parametrize("fuse", ["0", "1"])
 def test_sweep_pt_contraction_modes(monkeypatch, pt_mode, bt, N, chi, fuse):
     """PT contraction on the VALU (0), on the matrix cores (1, v_mfma_f64_4x4x4_4b; 3, split-complex
     v_mfma_f64_16x16x4 at B = 8) and mixed per wave (2)"""
     if bt == 8 and N > 4:
         pytest.skip("B=8 workgroups are built for N^2 <= 16")
+    if bt == 8 and chi > 64:
+        pytest.skip("chi = 128 runs B=4 workgroups (LDS)")
     monkeypatch.setenv("PQD_BT", str(bt))
     monkeypatch.setenv("PQD_PT_MODE", str(pt_mode))
     monkeypatch.setenv("PQD_FUSE", fuse)
