@@ -115,11 +115,13 @@ def export_csv(filename, *arg, precision=4, delimit=",", verbose=False):
 
 # ----------------------------------------------------------------------------- density matrices
 def concurrence(rho):
-    """Wootters concurrence of a two-qubit density matrix."""
+    """Wootters concurrence of a two-qubit density matrix (tools.py:167-172). A non-physical input with a negative
+    eigenvalue of rho T rho* T gives NaN, as in the reference (np.max propagates it; builtin max would not)."""
     flip = np.fliplr(np.diag([-1.0, 1.0, 1.0, -1.0]))
     R = rho @ flip @ np.conjugate(rho) @ flip
-    lam = np.sqrt(np.sort(np.real(np.linalg.eigvals(R))))
-    return max(0.0, lam[-1] - np.sum(lam[:-1]))
+    with np.errstate(invalid="ignore"):
+        lam = np.sqrt(np.sort(np.real(np.linalg.eigvals(R))))
+    return np.max([0.0, lam[-1] - np.sum(lam[:-1])])
 
 
 def compose_dm(outputs, dim=2):

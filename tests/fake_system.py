@@ -1,0 +1,46 @@
+"""A deterministic stand-in for a pyaceqd model function (tls / biexciton / sixls_linear) — TEST INFRASTRUCTURE.
+
+The caller modules (pol_entanglement.G2, two_time.*) only slice, integrate and combine what the model returns. To
+pin that bookkeeping against the reference's own code, tests/golden/make_golden.py runs the reference classes with
+`fake_system` in place of the ACE-backed model, and tests run ours with the same function. Every output row is an
+analytic function of time, of the operator string and of the multi-time operators that have acted, so an index
+slip or a swapped operator changes the numbers.
+
+It accepts both call forms: the reference's one-trajectory call (returns [t, <op_1>, ..., <op_n>]) and the batched
+`trajectories=[{"multitime_op", "t_end", "out_begin"}]` form of pyaceqd_amd.general_system (returns one
+(1 + n_out, window) array per trajectory, window = steps out_begin..round(t_end/dt)).
+"""
+import numpy as np
+
+
+def _h(s):
+    return (sum((i + 1) * ord(c) for i, c in enumerate(str(s))) % 997) / 997.0
+
+
+def fake_series(op, t, mtos):
+    a = _h(op)
+    v = (1 + a) * np.exp(-0.01 * (1 + a) * t) * np.exp(1j * (0.3 + a) * t)
+    for m in mtos:
+        tm = float(m["time"])
+        b = _h(str(m["operator"]) + str(m.get("applyFrom", "")))
+        on = (t >= tm - 1e-9).astype(float)
+        v = v + on * (0.5 + b) * np.exp(-0.02 * (t - tm)) * np.exp(1j * b * (t - tm)) * (1 + 0.1 * tm)
+    return v
+
+
+def _run(t_start, t_end, dt, mtos, output_ops):
+    n = int(round((t_end - t_start) / dt))
+    t = t_start + dt * np.arange(n + 1)
+    if isinstance(mtos, dict):
+        mtos = [mtos]
+    return np.array([t.astype(complex)] + [fake_series(o, t, mtos or []) for o in output_ops])
+
+
+def fake_system(t_start, t_end, *pulses, dt=0.1, multitime_op=None, output_ops=[], trajectories=None, **kw):
+    if trajectories is None:
+        return _run(t_start, t_end, dt, multitime_op, output_ops)
+    res = []
+    for spec in trajectories:
+        full = _run(t_start, spec.get("t_end", t_end), dt, spec.get("multitime_op"), output_ops)
+        res.append(full[:, int(spec.get("out_begin", 0)):])
+    return res

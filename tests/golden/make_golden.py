@@ -186,10 +186,54 @@ def gen_pyref():
                         tl_maps=tl, **ops_dm)
 
 
+def gen_polent():
+    """pol_entanglement.G2 bookkeeping: the REFERENCE class (pyaceqd/pol_entanglement/G2.py) driven by the
+    deterministic tests/fake_system.py model instead of ACE; our class runs on the same model in
+    tests/test_callers_golden.py."""
+    import tempfile
+    import warnings
+    warnings.simplefilter("ignore")
+    sys.path.insert(0, REF_ROOT)
+    from pyaceqd.pol_entanglement.G2 import PolarizatzionEntanglement as RefPE  # noqa: E402
+    from pyaceqd.pulses import ChirpedPulse  # noqa: E402
+    from tests.fake_system import fake_system  # noqa: E402
+    tmp = tempfile.mkdtemp() + "/"
+    p1 = ChirpedPulse(tau_0=1.0, e_start=1.0, alpha=0, e0=2.0, t0=5)
+    opts = {"gamma_e": 1 / 100, "temp_dir": tmp, "lindblad": True}
+    ops = ("|0><1|_4", "|0><2|_4", "|1><0|_4", "|2><0|_4")
+    out = {}
+    for tag, kw in {"ct": dict(dt=0.1, tend=14.0, dt_small=0.1), "reg": dict(dt=0.1, tend=6.0, dt_small=0.3,
+                                                                             regular_grid=True)}.items():
+        pe = RefPE(fake_system, *ops, p1, options=opts, **kw)
+        out[f"{tag}_t1"] = pe.t1
+        t1, t2, g, gi, full = pe.G2_reuse(pe.axdag, [pe.axdag + " * " + pe.ax, pe.aydag + " * " + pe.ay], pe.ax,
+                                          return_full_G2=True)
+        out.update({f"{tag}_reuse_t2": t2, f"{tag}_reuse_g": g, f"{tag}_reuse_int": gi, f"{tag}_reuse_full": full})
+        _, g2, g2i = pe.G2(pe.axdag, pe.aydag, pe.ay, pe.ax)
+        out.update({f"{tag}_g2": g2, f"{tag}_g2_int": np.array(g2i)})
+        c, rho = pe.calc_densitymatrix_reuse(return_rho=True)
+        out.update({f"{tag}_dm_reuse_c": np.array(c), f"{tag}_dm_reuse_rho": rho})
+        out[f"{tag}_dm_c"] = np.array(pe.calc_densitymatrix(), dtype=complex)
+        _, tt2, G1 = pe.G1(pe.ax, pe.axdag)
+        out.update({f"{tag}_g1_t2": tt2, f"{tag}_g1": G1})
+        fr, sp, sps = pe.get_spectrum(pe.ax, pe.axdag)
+        out.update({f"{tag}_spec_f": fr, f"{tag}_spec": sp, f"{tag}_spectra0": sps[0]})
+        for mode in ("t", "tau"):
+            r = pe.calc_timedependent_rho(mode=mode, add_norm=0.05, skip=1, return_G2=True)
+            for name, v in zip(("t", "c_t", "rho", "norm", "rho_int", "c_int", "G2_t"), r):
+                out[f"{tag}_tdr_{mode}_{name}"] = np.asarray(v)
+    np.savez_compressed(os.path.join(HERE, "pyref_polent.npz"), **out)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1:
+        for name in sys.argv[1:]:
+            globals()["gen_" + name]()
+        raise SystemExit(0)
     if not fref.available():
         raise SystemExit("build oracle/_ref first: make -C oracle ref")
     gen_fortran()
     gen_pyref()
+    gen_polent()
     tot = sum(os.path.getsize(os.path.join(HERE, f)) for f in os.listdir(HERE) if f.endswith(".npz"))
     print(f"golden fixtures written: {tot/1e6:.2f} MB")

@@ -413,3 +413,30 @@ def test_biexciton_generated_pt_two_time_vs_oracle(monkeypatch, tmp_path):
     _oracle_patch(monkeypatch)
     _, _, Gr = three_op_two_time(biexciton, t_axis, p, options=opts(), **kw)
     assert rel(G, Gr) < 1e-10
+
+
+# --------------------------------------------------------------------------------- pol-entanglement tomography
+def test_pol_entanglement_biexciton_vs_oracle(monkeypatch, tmp_path):
+    """PolarizatzionEntanglement on the biexciton cascade (two-photon excitation, fine-structure splitting) through
+    the batched driver: GPU vs the oracle for the 10-component density matrix and the time-resolved concurrence;
+    the physics gives a strongly entangled, fine-structure-degraded state (0 < C < 1)"""
+    from pyaceqd_amd.four_level_system.linear import biexciton
+    from pyaceqd_amd.pol_entanglement.G2 import PolarizatzionEntanglement
+    from pyaceqd_amd.pulses import ChirpedPulse
+    p = ChirpedPulse(tau_0=2.0, e_start=-2.0, e0=np.sqrt(2) * 1.0, t0=8)   # TPE at delta_b = 4 meV
+
+    def run():
+        opts = {"gamma_e": 1 / 50, "lindblad": True, "delta_xy": 0.005, "temp_dir": str(tmp_path) + "/"}
+        pe = PolarizatzionEntanglement(biexciton, "|0><1|_4+|1><3|_4", "|0><2|_4+|2><3|_4",
+                                       "|1><0|_4+|3><1|_4", "|2><0|_4+|3><2|_4", p, dt=0.1, tend=40,
+                                       regular_grid=True, dt_small=0.5, options=opts)
+        c, rho = pe.calc_densitymatrix_reuse(return_rho=True)
+        t1, t2, F = pe.calc_timedep_data()
+        t, c_t = pe.calc_timedependent_rho(t1=t1, t2=t2, G2_full=F, mode="tau")[:2]
+        return c, rho, F, c_t
+    c, rho, F, c_t = run()
+    _oracle_patch(monkeypatch)
+    cr, rhor, Fr, c_tr = run()
+    assert rel(rho, rhor) < 1e-10 and rel(F, Fr) < 1e-10
+    assert abs(c - cr) < 1e-9 and np.max(np.abs(c_t - c_tr)) < 1e-8
+    assert 0.3 < c < 1.0
