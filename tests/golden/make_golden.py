@@ -225,6 +225,78 @@ def gen_polent():
     np.savez_compressed(os.path.join(HERE, "pyref_polent.npz"), **out)
 
 
+def _ref_with_fortran_module():
+    """import path for reference modules that pull in the ACE-backed driver: pyaceqd/two_time/purity.py imports
+    `tls` and two correlation functions at module level (purity.py:13-14) that the golden scenarios never call; their
+    modules need the absent ACEutils library (general_system.py:14). Those two import targets are replaced by
+    placeholders that raise if called, so nothing of ACE is imitated; the model is tests/fake_system.py. The f2py
+    module `pyaceqd.two_time.propagate_tau_module` is provided by the reference's OWN Fortran compiled from
+    propagate_tau.f90 (oracle/fref.py), i.e. the real reference arithmetic."""
+    import types
+    sys.path.insert(0, REF_ROOT)
+
+    def _never(*a, **k):
+        raise RuntimeError("not available offline (needs ACE)")
+    for mod, names in {"pyaceqd.two_level_system.tls": ["tls"],
+                       "pyaceqd.two_time.correlations": ["tl_two_op_two_time", "tl_three_op_two_time"]}.items():
+        m = types.ModuleType(mod)
+        for n in names:
+            setattr(m, n, _never)
+        sys.modules[mod] = m
+    ptm = types.ModuleType("pyaceqd.two_time.propagate_tau_module")
+    for name in ("propagate_tau", "calc_onetime_parallel", "calc_onetime_parallel_block", "calc_twotime_phonon_block"):
+        setattr(ptm, name, getattr(fref, name))
+    sys.modules["pyaceqd.two_time.propagate_tau_module"] = ptm
+
+
+def gen_purity():
+    """two_time/purity.py bookkeeping and time-local-map paths: the REFERENCE Purity / Indistinguishability classes
+    driven by tests/fake_system.fake_system_dm (analytic outputs + synthetic dynamical maps), with the reference
+    Fortran behind propagate_tau_module; ours runs the same model in tests/test_callers_golden.py (GPU sweeps in
+    tests/test_gpu_parity.py)."""
+    import tempfile
+    import warnings
+    warnings.simplefilter("ignore")
+    _ref_with_fortran_module()
+    from pyaceqd.two_time.purity import Purity, Indistinguishability  # noqa: E402
+    from pyaceqd.pulses import ChirpedPulse  # noqa: E402
+    from tests.fake_system import fake_system_dm  # noqa: E402
+    tmp = tempfile.mkdtemp() + "/"
+    p = ChirpedPulse(tau_0=1.5, e_start=0, e0=1, t0=6)
+    kw = dict(dt=0.1, tb=20, dt_small=0.5, gaussian_t=12)
+    out = {}
+    pu = Purity(fake_system_dm, "|0><1|_2", "|1><0|_2", p, options={"gamma_e": 0.01, "temp_dir": tmp}, **kw)
+    out["pu_t1"] = pu.t1
+    t1, t2, G = pu.G2(return_whole=True)
+    out.update({"pu_g2_t2": t2, "pu_g2_whole": G})
+    out["pu_g2"] = pu.G2()[1]
+    out["pu_g2mod"] = pu.G2_modified("|1><1|_2")[1]
+    out["pu_purity"] = np.array(pu.calc_purity())
+    ind = Indistinguishability(fake_system_dm, "|0><1|_2", "|1><0|_2", p, options={"gamma_e": 0.01, "temp_dir": tmp},
+                               **kw)
+    out["in_g1"] = ind.G1()[1]
+    out["in_g0"] = ind.simple_propagation()[1]
+    out["in_indist"] = np.array(ind.calc_indistinguishability())
+    opts = {"gamma_e": 0.01, "temp_dir": tmp, "phonons": False}
+    tl = Indistinguishability(fake_system_dm, "|0><1|_2", "|1><0|_2", p, options=opts, dm=True, **kw)
+    tl.get_tl()
+    out.update({"tl_map": tl.tl_map, "tl_dms": tl.tl_dms})
+    out["tl_g0"] = tl.simple_propagation_tl()[1]
+    tt, rho = tl.calc_timedynamics_tl()
+    out.update({"tl_dyn_t": tt, "tl_dyn_rho": rho, "tl_complete": tl.tl_complete})
+    out["tl_g1"] = tl.G1_tl()[1]
+    out["tl_g2"] = tl.G2_tl()[1]
+    out["tl_indist"] = np.array(tl.calc_indistinguishability())
+    opts = {"gamma_e": 0.01, "temp_dir": tmp, "phonons": True}
+    ph = Indistinguishability(fake_system_dm, "|0><1|_2", "|1><0|_2", p, options=opts, dm=True, t_mem=2, **kw)
+    out["ph_g0"] = ph.simple_propagation_tl_phonons()[1]
+    tt, rho = ph.calc_timedynamics_tl_phonons()
+    out.update({"ph_dyn_t": tt, "ph_dyn_rho": rho})
+    out["ph_g1"] = ph.G1_tl_phonons()[1]
+    out["ph_g2"] = ph.G2_tl_phonons()[1]
+    np.savez_compressed(os.path.join(HERE, "pyref_purity.npz"), **out)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1:
         for name in sys.argv[1:]:
@@ -235,5 +307,6 @@ if __name__ == "__main__":
     gen_fortran()
     gen_pyref()
     gen_polent()
+    gen_purity()
     tot = sum(os.path.getsize(os.path.join(HERE, f)) for f in os.listdir(HERE) if f.endswith(".npz"))
     print(f"golden fixtures written: {tot/1e6:.2f} MB")

@@ -440,3 +440,45 @@ def test_pol_entanglement_biexciton_vs_oracle(monkeypatch, tmp_path):
     assert rel(rho, rhor) < 1e-10 and rel(F, Fr) < 1e-10
     assert abs(c - cr) < 1e-9 and np.max(np.abs(c_t - c_tr)) < 1e-8
     assert 0.3 < c < 1.0
+
+
+# --------------------------------------------------------------------------------- purity / indistinguishability
+def test_indistinguishability_map_sweeps_vs_reference_golden(golden_dir, tmp_path):
+    """Indistinguishability(dm=True) G1_tl / G2_tl (calc_onetime_parallel_block) and the phonon variants
+    (calc_twotime_phonon_block) on the GPU map-chain kernels vs the reference classes running the reference Fortran
+    on the same synthetic maps (tests/golden/pyref_purity.npz, tests/golden/make_golden.py gen_purity)"""
+    from pyaceqd_amd.pulses import ChirpedPulse
+    from pyaceqd_amd.two_time.purity import Indistinguishability
+    from tests.fake_system import fake_system_dm
+    z = np.load(os.path.join(golden_dir, "pyref_purity.npz"))
+    p = ChirpedPulse(tau_0=1.5, e_start=0, e0=1, t0=6)
+    kw = dict(dt=0.1, tb=20, dt_small=0.5, gaussian_t=12)
+    opts = {"gamma_e": 0.01, "temp_dir": str(tmp_path) + "/", "phonons": False}
+    tl = Indistinguishability(fake_system_dm, "|0><1|_2", "|1><0|_2", p, options=opts, dm=True, **kw)
+    assert rel(tl.G1_tl()[1], z["tl_g1"]) < 1e-11
+    assert rel(tl.G2_tl()[1], z["tl_g2"]) < 1e-11
+    assert np.max(np.abs(np.array(tl.calc_indistinguishability()) - z["tl_indist"])) < 1e-10
+    opts["phonons"] = True
+    ph = Indistinguishability(fake_system_dm, "|0><1|_2", "|1><0|_2", p, options=opts, dm=True, t_mem=2, **kw)
+    assert rel(ph.G1_tl_phonons()[1], z["ph_g1"]) < 1e-11
+    assert rel(ph.G2_tl_phonons()[1], z["ph_g2"]) < 1e-11
+
+
+def test_purity_tls_driver_vs_oracle(monkeypatch, tmp_path):
+    """Purity on the real TLS driver (pulse train, batched G2 trajectories): GPU vs oracle; a resonant pi pulse
+    much shorter than the lifetime gives a high single-photon purity (re-excitation keeps it below 1)"""
+    from pyaceqd_amd.pulses import ChirpedPulse
+    from pyaceqd_amd.two_level_system.tls import tls
+    from pyaceqd_amd.two_time.purity import Purity
+
+    def run():
+        pu = Purity(tls, "|0><1|_2", "|1><0|_2", ChirpedPulse(tau_0=1.0, e_start=0, e0=1, t0=5), dt=0.1, tb=60,
+                    dt_small=0.5, gaussian_t=10, options={"gamma_e": 1 / 10, "lindblad": True,
+                                                          "temp_dir": str(tmp_path) + "/"})
+        t2, g2 = pu.G2()
+        return g2, pu.calc_purity()
+    g2, P = run()
+    _oracle_patch(monkeypatch)
+    g2r, Pr = run()
+    assert rel(g2, g2r) < 1e-10 and abs(P - Pr) < 1e-10
+    assert 0.8 < P < 1.0
