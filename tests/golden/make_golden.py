@@ -297,6 +297,24 @@ def gen_purity():
     np.savez_compressed(os.path.join(HERE, "pyref_purity.npz"), **out)
 
 
+def gen_g1():
+    """two_time/G1.py G1_general bookkeeping: the REFERENCE function on tests/fake_system.fake_system"""
+    import warnings
+    warnings.simplefilter("ignore")
+    _ref_with_fortran_module()
+    from pyaceqd.two_time.G1 import G1_general  # noqa: E402
+    from pyaceqd.pulses import ChirpedPulse  # noqa: E402
+    from tests.fake_system import fake_system  # noqa: E402
+    p = ChirpedPulse(tau_0=1.0, e_start=0, e0=2, t0=4)
+    mto = {"operator": "|0><1|_2", "applyFrom": "_left", "applyBefore": "false"}
+    opts = {"phonons": False, "output_ops": ["|1><1|_2", "|1><0|_2"], "gamma_e": 0.01}
+    out = {}
+    for tag, kw in {"fine": dict(coarse_t=False), "coarse": dict(coarse_t=True, simple_exp=False)}.items():
+        t, tau, G = G1_general(0, 12, 0, 6, 0.5, 0.1, p, p, system=fake_system, multitime_op=mto, **kw, **opts)
+        out.update({f"{tag}_t": t, f"{tag}_tau": tau, f"{tag}_G": G})
+    np.savez_compressed(os.path.join(HERE, "pyref_g1.npz"), **out)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1:
         for name in sys.argv[1:]:
@@ -308,5 +326,6 @@ if __name__ == "__main__":
     gen_pyref()
     gen_polent()
     gen_purity()
+    gen_g1()
     tot = sum(os.path.getsize(os.path.join(HERE, f)) for f in os.listdir(HERE) if f.endswith(".npz"))
     print(f"golden fixtures written: {tot/1e6:.2f} MB")

@@ -482,3 +482,22 @@ def test_purity_tls_driver_vs_oracle(monkeypatch, tmp_path):
     g2r, Pr = run()
     assert rel(g2, g2r) < 1e-10 and abs(P - Pr) < 1e-10
     assert 0.8 < P < 1.0
+
+
+def test_g1_twols_and_mollow_vs_oracle(monkeypatch, tmp_path):
+    """G1_twols (batched t grid) and a two-area pulsed Mollow spectrum on the TLS driver: GPU vs oracle"""
+    from pyaceqd_amd.pulses import ChirpedPulse
+    from pyaceqd_amd.two_time import G1 as g1mod
+    td = str(tmp_path) + "/"
+
+    def run():
+        t, tau, g = g1mod.G1_twols(0, 20, 0, 10, 0.5, 0.1, ChirpedPulse(tau_0=1.0, e_start=0, e0=3, t0=5),
+                                   gamma_e=1 / 20, temp_dir=td)
+        f, a, s = g1mod.pulsed_mollow_tls(1.0, [1.0, 3.0], tend=20, tauend=10, dt=0.5, dtau=0.1, gamma_e=1 / 20,
+                                          temp_dir=td)
+        return g, s
+    g, s = run()
+    _oracle_patch(monkeypatch)
+    gr, sr = run()
+    assert rel(g, gr) < 1e-10 and rel(s, sr) < 1e-10
+    assert abs(g[0, 0]) < 1e-12                      # nothing excited before the pulse
