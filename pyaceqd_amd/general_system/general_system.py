@@ -168,8 +168,9 @@ def system_ace_stream(t_start, t_end, *pulses, dt=0.01, phonons=False, t_mem=20.
 
     Returns (1 + len(output_ops), n_t) complex, row 0 = time (general_system.py:104-110, 343).
     With calc_dynmap: (result, dm) with dm[i] = E(t_{i+1}, t_start) acting on row-major vec(rho)
-    (general_system.py:313-336, 358-359). With `trajectories` (list of dicts with keys
-    "multitime_op" and "t_end"): a list of per-trajectory results, all propagated in one launch.
+    (general_system.py:313-336, 358-359). With `trajectories` (list of dicts with keys "multitime_op", "t_end",
+    optionally "out_begin" and a per-trajectory drive "pulses" / "pulse_file_x" / "pulse_file_y"): a list of
+    per-trajectory results, all propagated in one launch (one System per distinct drive: parameter scans).
     """
     sanity_checks(system_op, phonons, boson_op, initial, interaction_ops, verbose)
     if multitime_op is not None:
@@ -223,51 +224,67 @@ def system_ace_stream(t_start, t_end, *pulses, dt=0.01, phonons=False, t_mem=20.
     # ---------------------------------------------------------------- pulse channels
     ds = dt / (4 * n_sub)
     ts = t_start + ds * np.arange(4 * n_sub * n_steps + 1)
-    channels, t0s, dts = [], [], []
-    use_pulses = [pulses[0]] if (firstonly and pulses) else list(pulses)
-    if rf_op is not None and rf_file is None:
-        use_pulses = _rf_pulses(use_pulses)
 
-    def add_channel(op_str, scale, t_s, f):
-        channels.append((scale * mat(op_str), np.asarray(f, dtype=complex)))
-        t0s.append(t_s[0])
-        dts.append(t_s[1] - t_s[0] if len(t_s) > 1 else ds)
+    def make_system(pulse_list, pfx, pfy):
+        channels, t0s, dts = [], [], []
+        use_pulses = [pulse_list[0]] if (firstonly and pulse_list) else list(pulse_list)
+        if rf_op is not None and rf_file is None:
+            use_pulses = _rf_pulses(use_pulses)
 
-    if interaction_ops:
-        fx = fy = None
-        tx = ty = ts
-        if pulse_file_x is not None:
-            tx, fx = read_pulse_file(pulse_file_x)
-        if pulse_file_y is not None:
-            ty, fy = read_pulse_file(pulse_file_y)
-        if fx is None or fy is None:
-            sx, sy = _sample_pulses(use_pulses, ts)
-            if fx is None:
-                fx = sx
-            if fy is None:
-                fy = sy
-        for op, pol in interaction_ops:
-            if pol == "y":
-                add_channel(op, -0.5 * np.pi * hbar, ty, fy)
+        def add_channel(op_str, scale, t_s, f):
+            channels.append((scale * mat(op_str), np.asarray(f, dtype=complex)))
+            t0s.append(t_s[0])
+            dts.append(t_s[1] - t_s[0] if len(t_s) > 1 else ds)
+
+        if interaction_ops:
+            fx = fy = None
+            tx = ty = ts
+            if pfx is not None:
+                tx, fx = read_pulse_file(pfx)
+            if pfy is not None:
+                ty, fy = read_pulse_file(pfy)
+            if fx is None or fy is None:
+                sx, sy = _sample_pulses(use_pulses, ts)
+                if fx is None:
+                    fx = sx
+                if fy is None:
+                    fy = sy
+            for op, pol in interaction_ops:
+                if pol == "y":
+                    add_channel(op, -0.5 * np.pi * hbar, ty, fy)
+                else:
+                    add_channel(op, -0.5 * np.pi * hbar, tx, fx)
+        if rf_op is not None:
+            if rf_file is not None:
+                tr, fr = read_pulse_file(rf_file)
             else:
-                add_channel(op, -0.5 * np.pi * hbar, tx, fx)
-    if rf_op is not None:
-        if rf_file is not None:
-            tr, fr = read_pulse_file(rf_file)
-        else:
-            tr, fr = ts, np.asarray(pulses[0].get_frequency(ts), dtype=complex) * np.ones_like(ts)
-        add_channel(rf_op, -0.5 * hbar, tr, fr)
-    # all channels must share one sample grid: resample onto the finest common raster if needed
-    if channels and (len(set(np.round(t0s, 12))) > 1 or len(set(np.round(dts, 12))) > 1
-                     or len({len(f) for _, f in channels}) > 1):
-        res = []
-        for (X, f), t0c, dtc in zip(channels, t0s, dts):
-            tc = t0c + dtc * np.arange(len(f))
-            res.append((X, np.interp(ts, tc, f.real) + 1j * np.interp(ts, tc, f.imag)))
-        channels = res
-        t0s, dts = [ts[0]], [ds]
-    system = System(dim=dim, H0=H0, lindblad=lind, channels=channels,
-                    sample_t0=t0s[0] if channels else 0.0, sample_dt=dts[0] if channels else 1.0)
+                tr, fr = ts, np.asarray(pulse_list[0].get_frequency(ts), dtype=complex) * np.ones_like(ts)
+            add_channel(rf_op, -0.5 * hbar, tr, fr)
+        # all channels must share one sample grid: resample onto the finest common raster if needed
+        if channels and (len(set(np.round(t0s, 12))) > 1 or len(set(np.round(dts, 12))) > 1
+                         or len({len(f) for _, f in channels}) > 1):
+            res = []
+            for (X, f), t0c, dtc in zip(channels, t0s, dts):
+                tc = t0c + dtc * np.arange(len(f))
+                res.append((X, np.interp(ts, tc, f.real) + 1j * np.interp(ts, tc, f.imag)))
+            channels = res
+            t0s, dts = [ts[0]], [ds]
+        return System(dim=dim, H0=H0, lindblad=lind, channels=channels,
+                      sample_t0=t0s[0] if channels else 0.0, sample_dt=dts[0] if channels else 1.0)
+
+    # per-trajectory drive (scans): a spec may carry its own "pulses" / "pulse_file_x" / "pulse_file_y"; every
+    # distinct drive becomes one System of a multi-system launch (engine.propagate, traj.system)
+    sys_keys, systems, traj_sys = {}, [], []
+    for spec in traj_specs:
+        pl = tuple(spec["pulses"]) if "pulses" in spec else tuple(pulses)
+        pfx = spec.get("pulse_file_x", pulse_file_x)
+        pfy = spec.get("pulse_file_y", pulse_file_y)
+        key = (tuple(id(p) for p in pl), pfx, pfy)
+        if key not in sys_keys:
+            sys_keys[key] = len(systems)
+            systems.append(make_system(pl, pfx, pfy))
+        traj_sys.append(sys_keys[key])
+    system = systems[0]
 
     if get_M_t is not None:
         g1 = Grid(get_M_t, dt, 1, n_sub)
@@ -299,9 +316,10 @@ def system_ace_stream(t_start, t_end, *pulses, dt=0.01, phonons=False, t_mem=20.
         n_real = 0
     else:
         n_real = len(out_mats)
-    tr = Trajectories(np.array(begins), np.array(ends), mtos)
+    multi = len(systems) > 1
+    tr = Trajectories(np.array(begins), np.array(ends), mtos, system=np.array(traj_sys) if multi else None)
     from .. import _lib
-    outs = propagate(system, grid, rho_init, out_mats, tr, pt=pt, ctx=_lib.context(device))
+    outs = propagate(systems if multi else system, grid, rho_init, out_mats, tr, pt=pt, ctx=_lib.context(device))
     results = []
     for k, o in enumerate(outs):
         steps = np.arange(begins[k], ends[k] + 1)
