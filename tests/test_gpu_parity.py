@@ -501,3 +501,33 @@ def test_g1_twols_and_mollow_vs_oracle(monkeypatch, tmp_path):
     gr, sr = run()
     assert rel(g, gr) < 1e-10 and rel(s, sr) < 1e-10
     assert abs(g[0, 0]) < 1e-12                      # nothing excited before the pulse
+
+
+# --------------------------------------------------------------------------------- scans (multi-system launches)
+def test_rabi_rotation_scan_one_launch(monkeypatch, tmp_path):
+    """RabiRotations: the whole area scan is one multi-system launch; final populations follow sin^2(pi A / 2)
+    (resonant, no decay), the emitted-photon scan matches the oracle"""
+    from pyaceqd_amd.two_level_system.rabi_rotations import RabiRotations
+    rr = RabiRotations(dt=0.05, tau=2, area_max=3, n_area=7, temp_dir=str(tmp_path) + "/")
+    areas, x = rr.get_rabi_rotations(integrate=False, path=str(tmp_path / "a_"), delete_pt=False)
+    assert np.max(np.abs(x - np.sin(np.pi * areas / 2) ** 2)) < 1e-5
+    rr2 = RabiRotations(dt=0.1, tau=2, area_max=3, n_area=5, gamma_e=1 / 50, temp_dir=str(tmp_path) + "/")
+    _, n_ph = rr2.get_rabi_rotations(integrate=True, path=str(tmp_path / "b_"), delete_pt=False)
+    _oracle_patch(monkeypatch)
+    rr3 = RabiRotations(dt=0.1, tau=2, area_max=3, n_area=5, gamma_e=1 / 50, temp_dir=str(tmp_path) + "/")
+    _, n_ref = rr3.get_rabi_rotations(integrate=True, path=str(tmp_path / "c_"), delete_pt=False)
+    assert np.max(np.abs(n_ph - n_ref)) < 1e-10
+    assert os.path.isfile(str(tmp_path / "b_rabi_.csv"))
+
+
+def test_tpe_rotation_scan_vs_oracle(monkeypatch, tmp_path):
+    from pyaceqd_amd.four_level_system.tpe_rotations import TPERotations
+
+    def run(tag):
+        tp = TPERotations(dt=0.1, tau=3, area_max=4, n_area=5, gamma_e=1 / 50, delta_b=4)
+        return tp.get_rabi_rotations(detuning=-2.0, integrate=False, path=str(tmp_path / tag), delete_pt=False)[1]
+    a = run("g_")
+    _oracle_patch(monkeypatch)
+    b = run("o_")
+    assert rel(a, b) < 1e-10
+    assert a[2].max() > 0.5            # two-photon resonant excitation reaches the biexciton
