@@ -432,7 +432,7 @@ def test_pol_entanglement_biexciton_vs_oracle(monkeypatch, tmp_path):
                                        regular_grid=True, dt_small=0.5, options=opts)
         c, rho = pe.calc_densitymatrix_reuse(return_rho=True)
         t1, t2, F = pe.calc_timedep_data()
-        t, c_t = pe.calc_timedependent_rho(t1=t1, t2=t2, G2_full=F, mode="t", skip=1)[:2]
+        t, c_t = pe.calc_timedependent_rho(t1=t1, t2=t2, G2_full=F, mode="t", skip=40)[:2]   # photons exist only after the pulse
         return c, rho, F, c_t
     c, rho, F, c_t = run()
     _oracle_patch(monkeypatch)
