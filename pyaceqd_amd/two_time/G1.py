@@ -117,7 +117,8 @@ def pulsed_mollow_tls(pulse_tau, areas, detuning=0, tend=500, tauend=500, dt=0.2
                       temperature=4, phonons=False, pt_file="tls_3.0nm_4k_th10_tmem20.48_dt0.02.ptr", workers=7,
                       temp_dir=temp_dir, save_dir=None, prepare_only=False, simple_exp=False, gaussian_t=False,
                       **ops):
-    """pulsed Mollow spectra of Gaussian pulses over pulse areas (reference :119-160)"""
+    """pulsed Mollow spectra of Gaussian pulses over pulse areas (reference :119-160). As in the reference, the
+    coarse_t=True call of G1_twols hands the single pulse to construct_t's dt_exp slot (:44-48), so this raises."""
     from ..pulses import ChirpedPulse
     n_tau = int(tauend / dtau)
     spectra = np.zeros([len(areas), 2 * (n_tau + 1) - 1])
