@@ -315,6 +315,78 @@ def gen_g1():
     np.savez_compressed(os.path.join(HERE, "pyref_g1.npz"), **out)
 
 
+def gen_twophoton():
+    """timebin/twophoton_new.py: the REFERENCE TwoPhotonTimebinNew on tests/fake_system.fake_system_dm. Its compiled
+    helper `pyaceqd.timebin.timebin_tl` is provided by the reference's own Fortran (four_time, four_time_8op via
+    oracle/fref.py); the two `utils` module functions the class calls from Python (fast_propagate, propagate_tb,
+    timebin_tl.f90:23-77, module procedures returning arrays, which a C binding cannot reach) are restated below in
+    numpy from that source."""
+    import tempfile
+    import types
+    import warnings
+    warnings.simplefilter("ignore")
+    _ref_with_fortran_module()
+
+    def fast_propagate(rho, pre, n_steps, dimsquare=None, n_precalc=None):
+        out, n, i = np.array(rho, dtype=complex), int(n_steps), 0
+        while n > 0:
+            if n & 1:
+                out = pre[:, :, i] @ out
+            n >>= 1
+            i += 1
+        return out
+
+    def propagate_tb(t_start, t_stop, dt, rho, dm_tl, pre, n_precalc=None, dimsquare=None, n_dm=None):
+        r6 = lambda x: np.rint(x * 1e6) / 1e6  # noqa: E731
+        n_start, n_stop = int(r6(t_start) / dt), int(r6(t_stop) / dt)
+        n_steps = n_stop - n_start
+        steps = min(dm_tl.shape[2] - n_start, n_steps)
+        out = np.array(rho, dtype=complex)
+        while steps > 0:
+            out = dm_tl[:, :, n_start] @ out
+            n_steps -= 1
+            n_start += 1
+            steps -= 1
+        return fast_propagate(out, pre, n_steps) if n_steps > 0 else out
+    tb_mod = types.ModuleType("pyaceqd.timebin.timebin_tl")
+    tb_mod.four_time = lambda dm_1, dm_2, rho_init, t1, precalc, dt, dim, o1, o2, o3, o4, tb: fref.four_time(
+        dm_1, dm_2, rho_init, t1, precalc, dt, dim, o1, o2, o3, o4, tb)
+    tb_mod.four_time_8op = lambda dm_1, dm_2, rho_init, t1, precalc, dt, dim, *rest: fref.four_time_8op(
+        dm_1, dm_2, rho_init, t1, precalc, dt, dim, rest[:8], rest[8], rest[9], rest[10])
+    tb_mod.utils = types.SimpleNamespace(fast_propagate=fast_propagate, propagate_tb=propagate_tb)
+    sys.modules["pyaceqd.timebin.timebin_tl"] = tb_mod
+    import pyaceqd.timebin as pkg  # noqa: E402
+    pkg.timebin_tl = tb_mod
+    from pyaceqd.timebin.twophoton_new import TwoPhotonTimebinNew  # noqa: E402
+    from pyaceqd.pulses import ChirpedPulse  # noqa: E402
+    from tests.fake_system import fake_system_dm  # noqa: E402
+    tmp = tempfile.mkdtemp() + "/"
+    ps = [ChirpedPulse(tau_0=1.0, e_start=0, e0=1, t0=3), ChirpedPulse(tau_0=1.0, e_start=0, e0=1, t0=15)]
+    ops = ("|0><1|_4", "|1><0|_4", "|1><3|_4", "|3><1|_4")
+    opts = {"gamma_e": 0.05, "temp_dir": tmp, "fake_dim": 4}
+    kw = dict(dt=0.1, dim=4, tb=12, dt_small=0.5, n_tbig=2, gaussian_t=6)
+    out = {}
+    tp = TwoPhotonTimebinNew(fake_system_dm, *ops, *ps, options=opts, **kw)
+    out["t1"] = tp.t1
+    c, rho = tp.calc_densitymatrix(reduced=False)
+    out.update({"dm_c": np.array(c), "dm_rho": rho})
+    r = tp.rho_ee_ee()
+    out.update({"eeee_G": r[2], "eeee_table": r[6]})
+    out["eell_table"] = tp.rho_ee_ll()[5]
+    out["elll_G1"], out["elll_G2"] = tp.rho_el_ll()[3:5]
+    tl = TwoPhotonTimebinNew(fake_system_dm, *ops, *ps, options=opts, **kw)
+    c, rho, rhon = tl.calc_densitymatrix_tl(reduced=False)
+    out.update({"tl_c": np.array(c), "tl_rho": rho})
+    out["tl_eell_f"] = tl.eell_tl_f()[3]
+    t, rho_t = tl.dynamics_tl()
+    out.update({"tl_dyn_t": t, "tl_dyn_rho": rho_t})
+    t, rho_t = tl.dynamics_tl_t1()
+    out.update({"tl_dyn1_t": t, "tl_dyn1_rho": rho_t})
+    ft = tl.four_time_tl(tp.sigma_bdag, tp.sigma_xdag, tp.sigma_b, tp.sigma_x)
+    out.update({"tl_ft_G": ft[1], "tl_ft_table": ft[3]})
+    np.savez_compressed(os.path.join(HERE, "pyref_twophoton.npz"), **out)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1:
         for name in sys.argv[1:]:
@@ -327,5 +399,6 @@ if __name__ == "__main__":
     gen_polent()
     gen_purity()
     gen_g1()
+    gen_twophoton()
     tot = sum(os.path.getsize(os.path.join(HERE, f)) for f in os.listdir(HERE) if f.endswith(".npz"))
     print(f"golden fixtures written: {tot/1e6:.2f} MB")
