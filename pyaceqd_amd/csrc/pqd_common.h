@@ -75,7 +75,9 @@ struct SweepParams {
     const double2* W;        // output rows through M_b(m-1): W(m) = ovec . M_b(m-1)   [n_sys][n_steps+1][n_out][N2]
     long long f_stride, w_stride;
     int fuse;                // 1: steps without MTOs apply F(m) once instead of M_b(m-1) then M_a(m)
-    int pt_mode;             // PT contraction: 0 VALU, 1 matrix cores (4x4x4_4b), 2 mixed per wave
+    int pt_mode;             // PT contraction: 0 VALU, 1 matrix cores (4x4x4_4b), 2 mixed per wave,
+                             //   3 split-complex 16x16x4 (BT = 8), 4 matrix cores with 3 real products (3M)
+    int cmul3;               // column phases with 3 real products per complex product (3M)
     int ablate;              // diagnostics only (PQD_ABLATE): 1 skip PT, 2 skip column phases, 4 skip outputs
 };
 

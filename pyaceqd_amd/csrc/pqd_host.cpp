@@ -528,7 +528,8 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     sp.blk_traj = P->blk_traj.p; sp.blk_end = P->blk_end.p; sp.blk_sys = P->blk_sys.p;
     sp.traj_sys = P->traj_sys.p; sp.m_stride = (long long)2 * ns * m2; sp.wbeg = P->wbeg.p; sp.wend = P->wend.p;
     { const char* ab = getenv("PQD_ABLATE"); sp.ablate = ab ? atoi(ab) : 0; }
-    { const char* pm = getenv("PQD_PT_MODE"); sp.pt_mode = pm ? atoi(pm) : 1; }
+    { const char* pm = getenv("PQD_PT_MODE"); sp.pt_mode = pm ? atoi(pm) : 4; }
+    { const char* c3 = getenv("PQD_CMUL3"); sp.cmul3 = c3 ? atoi(c3) : 1; }
     { const char* fz = getenv("PQD_FUSE"); sp.fuse = (!P->nopt && ns > 0 && (fz ? atoi(fz) : 1)) ? 1 : 0; }
     if (sp.fuse) {
         HIPCHK(P->F.alloc((size_t)n_sys * ns * m2));

@@ -97,6 +97,68 @@ __device__ __forceinline__ void col_apply_mfma(const double2* __restrict__ Op, d
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
+// Column phase with three real products per complex product ("3M"): P1 = Ar Br, P2 = Ai Bi,
+// P3 = (Ar + Ai)(Br + Bi); Cr = P1 - P2, Ci = P3 - P1 - P2. Three MFMA chains instead of four, the sums are
+// two VALU adds per operand fragment. Error bound eps (|Ar||Br| + |Ai||Bi| + |Ar + Ai||Br + Bi|) per product,
+// i.e. the same order as the 4M form for these O(1) propagators.
+template <int N2, int CHI, int RS>
+__device__ __forceinline__ void col_apply_mfma3(const double2* __restrict__ Op, double2* S, int lane) {
+    constexpr int MT = (N2 + 15) / 16;
+    constexpr int KS = (N2 + 3) / 4;
+    constexpr int NTL = CHI / 16;
+    constexpr bool CACHE_A = KS * MT <= 8;
+    const int li = lane & 15, lk = lane >> 4;
+    double2 ac[CACHE_A ? KS * MT : 1];
+    double as[CACHE_A ? KS * MT : 1];
+    if constexpr (CACHE_A) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+                const int r = 16 * mt + li, a = 4 * ks + lk;
+                ac[ks * MT + mt] = (r < N2 && a < N2) ? Op[r * N2 + a] : c_zero();
+                as[ks * MT + mt] = ac[ks * MT + mt].x + ac[ks * MT + mt].y;
+            }
+    }
+#pragma unroll
+    for (int nt = 0; nt < NTL; ++nt) {
+        dbl4 p1[MT], p2[MT], p3[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) { p1[mt] = dbl4{0, 0, 0, 0}; p2[mt] = p1[mt]; p3[mt] = p1[mt]; }
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int a = 4 * ks + lk;
+            const double2 b = (a < N2) ? S[a * RS + 16 * nt + li] : c_zero();
+            const double bs = b.x + b.y;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+                double2 m;
+                double ms;
+                if constexpr (CACHE_A) {
+                    m = ac[ks * MT + mt];
+                    ms = as[ks * MT + mt];
+                } else {
+                    const int r = 16 * mt + li;
+                    m = (r < N2 && a < N2) ? Op[r * N2 + a] : c_zero();
+                    ms = m.x + m.y;
+                }
+                p1[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(m.x, b.x, p1[mt], 0, 0, 0);
+                p2[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(m.y, b.y, p2[mt], 0, 0, 0);
+                p3[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(ms, bs, p3[mt], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 16 * mt + lk + 4 * r;
+                if (row < N2)
+                    S[row * RS + 16 * nt + li] = make_double2(p1[mt][r] - p2[mt][r], p3[mt][r] - p1[mt][r] - p2[mt][r]);
+            }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
 // PT contraction of one Liouville row alpha on the matrix cores (v_mfma_f64_4x4x4_4b_f64):
 //   C[BT x CHI] = X[BT x CHI] . Qg[CHI x CHI],  X = rows alpha of the BT trajectories.
 // gfx950 lane map of the 4-block f64 MFMA (measured): lane l = 16 k + 4 blk + x holds A[blk][x][k],
@@ -144,6 +206,52 @@ __device__ __forceinline__ void pt_row_mfma(const double2* __restrict__ Qg, doub
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
         for (int g = 0; g < NG; ++g) wr[(4 * rb + kk) * TS + 16 * g] = make_double2(cr[rb][g], ci[rb][g]);
+}
+
+// pt_row_mfma with three real products per complex product (3M, see col_apply_mfma3): 3 MFMA chains per
+// (row block, column group) instead of 4; (Qr + Qi) and (Xr + Xi) are one VALU add per loaded element.
+template <int CHI, int BT, int RS, int TS>
+__device__ __forceinline__ void pt_row_mfma3(const double2* __restrict__ Qg, double2* st, int a, int lane) {
+    constexpr int RB = BT / 4, NG = CHI / 16, KSN = CHI / 4;
+    const int x = lane & 3, kk = lane >> 4, c16 = lane & 15;
+    double p1[RB][NG], p2[RB][NG], p3[RB][NG];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int g = 0; g < NG; ++g) { p1[rb][g] = 0.0; p2[rb][g] = 0.0; p3[rb][g] = 0.0; }
+    const double2* xr = st + a * RS + kk;
+    const double2* qp = Qg + (size_t)kk * CHI + c16;
+    double2 qn[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) qn[g] = qp[16 * g];
+#pragma unroll 2
+    for (int ks = 0; ks < KSN; ++ks) {
+        double2 qv[NG];
+        double qs[NG];
+#pragma unroll
+        for (int g = 0; g < NG; ++g) { qv[g] = qn[g]; qs[g] = qv[g].x + qv[g].y; }
+        if (ks + 1 < KSN) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) qn[g] = qp[(size_t)4 * (ks + 1) * CHI + 16 * g];
+        }
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+            const double2 av = xr[(4 * rb + x) * TS + 4 * ks];
+            const double as = av.x + av.y;
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                p1[rb][g] = __builtin_amdgcn_mfma_f64_4x4x4f64(av.x, qv[g].x, p1[rb][g], 0, 0, 0);
+                p2[rb][g] = __builtin_amdgcn_mfma_f64_4x4x4f64(av.y, qv[g].y, p2[rb][g], 0, 0, 0);
+                p3[rb][g] = __builtin_amdgcn_mfma_f64_4x4x4f64(as, qs[g], p3[rb][g], 0, 0, 0);
+            }
+        }
+    }
+    double2* wr = st + a * RS + c16;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+            wr[(4 * rb + kk) * TS + 16 * g] = make_double2(p1[rb][g] - p2[rb][g], p3[rb][g] - p1[rb][g] - p2[rb][g]);
 }
 
 // PT contraction of row alpha for BT = 8 on v_mfma_f64_16x16x4_f64 ("split complex"): the 16 MFMA rows are
@@ -230,6 +338,11 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
     __syncthreads();
     // ---- column phases: wave w owns trajectory w (its free propagators, its MTO events)
     double2* stw = st + wave * TS;
+    const bool c3 = p.cmul3 != 0;
+    auto col = [&](const double2* __restrict__ Op) {
+        if (c3) col_apply_mfma3<N2, CHI, RS>(Op, stw, lane);
+        else col_apply_mfma<N2, CHI, RS>(Op, stw, lane);
+    };
     int ev_cur = 0, ev_lim = 0;
     {
         const int t = s_traj[wave];
@@ -237,7 +350,7 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
         while (ev_cur < ev_lim) {  // applyBefore-true MTOs at step 0
             const int4 e = p.ev[ev_cur];
             if (e.x != 0 || e.y != 0) break;
-            col_apply_mfma<N2, CHI, RS>(p.sop + (size_t)e.z * N2 * N2, stw, lane);
+            col(p.sop + (size_t)e.z * N2 * N2);
             ++ev_cur;
         }
     }
@@ -285,15 +398,15 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
         const double2* Ma = Mg + (size_t)(2 * n) * N2 * N2;
         if (!(p.ablate & 2)) {
             if (fz) {  // no MTO at step n: M_b(n-1) and M_a(n) in one operator
-                col_apply_mfma<N2, CHI, RS>(Fg + (size_t)n * N2 * N2, stw, lane);
+                col(Fg + (size_t)n * N2 * N2);
             } else {
                 while (ev_cur < ev_lim) {  // applyBefore-false MTOs at step n
                     const int4 e = p.ev[ev_cur];
                     if (e.x != n || e.y != 1) break;
-                    col_apply_mfma<N2, CHI, RS>(p.sop + (size_t)e.z * N2 * N2, stw, lane);
+                    col(p.sop + (size_t)e.z * N2 * N2);
                     ++ev_cur;
                 }
-                col_apply_mfma<N2, CHI, RS>(Ma, stw, lane);
+                col(Ma);
             }
         }
         __syncthreads();
@@ -301,13 +414,18 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
         // ------------------------------------------------------------ PT contraction
         if (!(p.ablate & 1)) {
             const double2* Qs = Qg0 + (size_t)p.sched[n] * p.D * CHI * CHI;
-            // pt_mode 0: VALU rows, 1: matrix-core rows (4x4x4_4b), 3: split-complex 16x16x4 rows (BT = 8), 2: mixed (waves 0..NW/2-1 start on the matrix cores,
+            // pt_mode 0: VALU rows, 1: matrix-core rows (4x4x4_4b), 4: matrix-core rows with 3 real products per
+            // complex product (default), 3: split-complex 16x16x4 rows (BT = 8), 2: mixed (waves 0..NW/2-1 start on the matrix cores,
             // the others on the VALU, alternating per row), so the two FP64 pipes of a SIMD run concurrently
             int parity = (p.pt_mode == 2) ? ((wave >= NW / 2) ? 1 : 0) : 0;
             for (int a = wave; a < N2; a += NW) {
                 const double2* Qg = Qs + (size_t)p.gmap[a] * CHI * CHI;
                 const bool use_mfma = (p.pt_mode == 1) || (p.pt_mode == 2 && parity == 0);
                 parity ^= 1;
+                if (p.pt_mode == 4) {
+                    pt_row_mfma3<CHI, BT, RS, TS>(Qg, st, a, lane);
+                    continue;
+                }
                 if constexpr (BT == 8) {
                     if (p.pt_mode == 3) {
                         pt_row_mfma16<CHI, RS, TS>(Qg, st, a, lane);
@@ -394,11 +512,11 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
         // fuse M_b(n) into the next step's operator unless this trajectory has an MTO at step n+1
         fz = p.fuse && !(ev_cur < ev_lim && p.ev[ev_cur].x == n + 1);
         if (!(p.ablate & 2) && !fz) {
-            col_apply_mfma<N2, CHI, RS>(Mb, stw, lane);
+            col(Mb);
             while (ev_cur < ev_lim) {  // applyBefore-true MTOs at step n+1
                 const int4 e = p.ev[ev_cur];
                 if (e.x != n + 1 || e.y != 0) break;
-                col_apply_mfma<N2, CHI, RS>(p.sop + (size_t)e.z * N2 * N2, stw, lane);
+                col(p.sop + (size_t)e.z * N2 * N2);
                 ++ev_cur;
             }
         }

@@ -348,13 +348,15 @@ def test_bench_workload_small_vs_oracle(monkeypatch, fuse):
     cmp_lists(got, ref, 1e-11)
 
 
-@pytest.mark.parametrize("pt_mode", [0, 1, 2, 3])
+@pytest.mark.parametrize("pt_mode", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("bt", [4, 8])
 @pytest.mark.parametrize("N,chi", [(2, 16), (3, 32), (4, 64), (5, 64), (6, 32), (2, 128), (4, 128)])
 @pytest.mark.parametrize("fuse", ["0", "1"])
 def test_sweep_pt_contraction_modes(monkeypatch, pt_mode, bt, N, chi, fuse):
-    """PT contraction on the VALU (0), on the matrix cores (1, v_mfma_f64_4x4x4_4b; 3, split-complex
-    v_mfma_f64_16x16x4 at B = 8) and mixed per wave (2)"""
+    """PT contraction on the VALU (0), on the matrix cores (1, v_mfma_f64_4x4x4_4b; 4, the same with three real
+    products per complex product; 3, split-complex v_mfma_f64_16x16x4 at B = 8) and mixed per wave (2); column
+    phases alternate between the 4M and 3M complex products"""
+    monkeypatch.setenv("PQD_CMUL3", str((pt_mode + bt + chi) % 2))
     if bt == 8 and N > 4:
         pytest.skip("B=8 workgroups are built for N^2 <= 16")
     if bt == 8 and chi > 64:
