@@ -210,7 +210,8 @@ __device__ __forceinline__ void pt_row_mfma(const double2* __restrict__ Qg, doub
 
 // pt_row_mfma with three real products per complex product (3M, see col_apply_mfma3): 3 MFMA chains per
 // (row block, column group) instead of 4; (Qr + Qi) and (Xr + Xi) are one VALU add per loaded element.
-template <int CHI, int BT, int RS, int TS>
+// PF = how many k-steps of the PT slice are in flight ahead of the MFMAs (L2 latency hiding).
+template <int CHI, int BT, int RS, int TS, int PF = 1>
 __device__ __forceinline__ void pt_row_mfma3(const double2* __restrict__ Qg, double2* st, int a, int lane) {
     constexpr int RB = BT / 4, NG = CHI / 16, KSN = CHI / 4;
     const int x = lane & 3, kk = lane >> 4, c16 = lane & 15;
@@ -221,18 +222,24 @@ __device__ __forceinline__ void pt_row_mfma3(const double2* __restrict__ Qg, dou
         for (int g = 0; g < NG; ++g) { p1[rb][g] = 0.0; p2[rb][g] = 0.0; p3[rb][g] = 0.0; }
     const double2* xr = st + a * RS + kk;
     const double2* qp = Qg + (size_t)kk * CHI + c16;
-    double2 qn[NG];
+    double2 qn[PF][NG];
 #pragma unroll
-    for (int g = 0; g < NG; ++g) qn[g] = qp[16 * g];
-#pragma unroll 2
+    for (int f = 0; f < PF; ++f)
+#pragma unroll
+        for (int g = 0; g < NG; ++g) qn[f][g] = qp[(size_t)4 * f * CHI + 16 * g];
+#pragma unroll PF + 1
     for (int ks = 0; ks < KSN; ++ks) {
         double2 qv[NG];
         double qs[NG];
 #pragma unroll
-        for (int g = 0; g < NG; ++g) { qv[g] = qn[g]; qs[g] = qv[g].x + qv[g].y; }
-        if (ks + 1 < KSN) {
+        for (int g = 0; g < NG; ++g) { qv[g] = qn[0][g]; qs[g] = qv[g].x + qv[g].y; }
 #pragma unroll
-            for (int g = 0; g < NG; ++g) qn[g] = qp[(size_t)4 * (ks + 1) * CHI + 16 * g];
+        for (int f = 0; f + 1 < PF; ++f)
+#pragma unroll
+            for (int g = 0; g < NG; ++g) qn[f][g] = qn[f + 1][g];
+        if (ks + PF < KSN) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) qn[PF - 1][g] = qp[(size_t)4 * (ks + PF) * CHI + 16 * g];
         }
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) {
@@ -423,7 +430,11 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
                 const bool use_mfma = (p.pt_mode == 1) || (p.pt_mode == 2 && parity == 0);
                 parity ^= 1;
                 if (p.pt_mode == 4) {
-                    pt_row_mfma3<CHI, BT, RS, TS>(Qg, st, a, lane);
+                    pt_row_mfma3<CHI, BT, RS, TS, 1>(Qg, st, a, lane);
+                    continue;
+                }
+                if (p.pt_mode == 5) {   // 3M with two k-steps of the slice in flight
+                    pt_row_mfma3<CHI, BT, RS, TS, 2>(Qg, st, a, lane);
                     continue;
                 }
                 if constexpr (BT == 8) {

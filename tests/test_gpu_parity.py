@@ -348,7 +348,7 @@ def test_bench_workload_small_vs_oracle(monkeypatch, fuse):
     cmp_lists(got, ref, 1e-11)
 
 
-@pytest.mark.parametrize("pt_mode", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("pt_mode", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("bt", [4, 8])
 @pytest.mark.parametrize("N,chi", [(2, 16), (3, 32), (4, 64), (5, 64), (6, 32), (2, 128), (4, 128)])
 @pytest.mark.parametrize("fuse", ["0", "1"])
