@@ -314,7 +314,7 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
     extern __shared__ __attribute__((aligned(16))) double2 smem[];
     double2* st = smem;
     double2* rbuf = smem + BT * TS;
-    __shared__ int s_traj[BT], s_wb[BT], s_we[BT];
+    __shared__ int s_traj[BT], s_wb[BT], s_we[BT], s_fz[BT];
     __shared__ long long s_wo[BT];
 
     const int tid = threadIdx.x;
@@ -327,6 +327,7 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
         s_wb[tid] = t >= 0 ? p.wbeg[t] : INT_MAX;
         s_we[tid] = t >= 0 ? p.wend[t] : -1;
         s_wo[tid] = t >= 0 ? p.woff[t] : 0;
+        s_fz[tid] = 0;
     }
     __syncthreads();
     const int n_end = p.blk_end[blockIdx.x];
@@ -365,34 +366,37 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
     const int pj = lane & 15, pq = lane >> 4;
     bool fz = false;  // this wave's trajectory sits between M_b(n-1) and M_a(n) unapplied (fused step n)
     for (int n = 0;; ++n) {
-        // ------------------------------------------------------------ outputs at step n (per wave)
-        // Wave w reads out its own trajectory: closure contraction of its N2 rows (4 lanes per row, xor-1/2
-        // shuffles), then the traces from its own rbuf slice. No other wave touches these data, so the phase
-        // needs no workgroup barrier (2 barriers per step instead of 4).
-        if (!(p.ablate & 4) && s_wb[wave] <= n && n <= s_we[wave]) {
+        // ------------------------------------------------------------ outputs at step n
+        bool need = false;
+#pragma unroll
+        for (int b = 0; b < BT; ++b) need |= (s_wb[b] <= n) & (n <= s_we[b]);
+        if (need && !(p.ablate & 4)) {
             const double2* cvec = (n == 0) ? p.closure0 : p.closure + (size_t)p.sched[n - 1] * CHI;
-            double2* rw = rbuf + wave * N2;
-            for (int e0 = 0; e0 < N2 * 4; e0 += 64) {
-                const int e = e0 + lane;
+            constexpr int NPART = BT * N2 * 4;
+            for (int it = 0; it < (NPART + NT - 1) / NT; ++it) {
+                const int e = tid + NT * it;
                 const int row = e >> 2, qr = e & 3;
-                double2 sacc = c_zero();
-                if (e < N2 * 4) {
-                    const double2* rp = stw + row * RS + qr;
+                double2 s = c_zero();
+                if (e < NPART) {
+                    const int b = row / N2, a = row - (row / N2) * N2;
+                    const double2* rp = st + b * TS + a * RS + qr;
 #pragma unroll 4
-                    for (int kk = 0; kk < CHI / 4; ++kk) c_fma(sacc, rp[4 * kk], cvec[4 * kk + qr]);
+                    for (int kk = 0; kk < CHI / 4; ++kk) c_fma(s, rp[4 * kk], cvec[4 * kk + qr]);
                 }
-                sacc = c_add(sacc, c_shfl_xor(sacc, 1));
-                sacc = c_add(sacc, c_shfl_xor(sacc, 2));
-                if (e < N2 * 4 && qr == 0) rw[row] = sacc;
+                s = c_add(s, c_shfl_xor(s, 1));
+                s = c_add(s, c_shfl_xor(s, 2));
+                if (e < NPART && qr == 0) rbuf[row] = s;
             }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            // fused trajectories still hold the state before M_b(n-1): read it through W(n)
-            const double2* ovb = fz ? Wg + (size_t)n * p.n_out * N2 : p.ovec;
-            for (int k = lane; k < p.n_out; k += 64) {
-                double2 sacc = c_zero();
-                const double2* ov = ovb + (size_t)k * N2;
-                for (int a = 0; a < N2; ++a) c_fma(sacc, ov[a], rw[a]);
-                outg[s_wo[wave] + (long long)(n - s_wb[wave]) * p.n_out + k] = sacc;
+            __syncthreads();
+            for (int e = tid; e < BT * p.n_out; e += NT) {
+                const int b = e / p.n_out, k = e - (e / p.n_out) * p.n_out;
+                if (s_wb[b] <= n && n <= s_we[b]) {
+                    double2 s = c_zero();
+                    // fused trajectories still hold the state before M_b(n-1): read it through W(n)
+                    const double2* ov = (s_fz[b] ? Wg + (size_t)n * p.n_out * N2 : p.ovec) + (size_t)k * N2;
+                    for (int a = 0; a < N2; ++a) c_fma(s, ov[a], rbuf[b * N2 + a]);
+                    outg[s_wo[b] + (long long)(n - s_wb[b]) * p.n_out + k] = s;
+                }
             }
         }
         if (n >= n_end) break;
@@ -527,8 +531,8 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
                 ++ev_cur;
             }
         }
-        // no barrier: the next outputs and column phase A touch only this wave's trajectory; the barrier
-        // after phase A orders them before the next PT phase
+        if (lane == 0) s_fz[wave] = fz ? 1 : 0;
+        __syncthreads();
     }
 }
 
