@@ -223,6 +223,8 @@ def main():
                      "kernel": "pt_sweep_kernel<16,64>",
                      "algorithmic": f"{F} flop/traj-step ({'fused' if fused else 'unfused'} half steps) x {executed} "
                                     f"executed traj-steps per launch",
+                     "flop_convention": "8 real flops per complex multiply-add (SURVEY.md §8d); with the default 3M "
+                                        "products (PQD_PT_MODE=4, PQD_CMUL3=1) the matrix cores execute 6",
                      "hbm_algorithmic_GBs": bytes_per_launch(grid.n_steps, 410, args.chi, n_traj=n_traj,
                                                              executed_steps=executed) / (ms_sweep * 1e-3) / 1e9},
     }

@@ -10,7 +10,7 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpqd.so")
+LIB_PATH = os.environ.get("PQD_LIB") or os.path.join(_HERE, "libpqd.so")  # PQD_LIB: A/B of builds
 
 
 class PQDError(RuntimeError):

@@ -3,7 +3,6 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
 crash() { case "$1" in 0|1|2|5) return 1;; *) return 0;; esac; }
-for v in ${VARIANTS:-"PQD_PT_MODE=4 PQD_CMUL3=1" "PQD_PT_MODE=1 PQD_CMUL3=0"}; do :; done
 i=0
 while IFS= read -r v; do
   [ -z "$v" ] && continue
