@@ -75,6 +75,8 @@ def flops_per_traj_step(N=4, chi=64, n_out=2, fused=True):
     fuses M_b(n-1) and M_a(n) into one N^2 x N^2 operator on steps without MTOs, so the
     executed algorithm does one column product per step: F_fused = 8 (D chi^2 + chi N^4 + n_out N^2)."""
     D = N * N
+    if chi <= 1:
+        return 8 * ((1 if fused else 2) * N ** 4 + n_out * N * N)
     return 8 * (D * chi * chi + (1 if fused else 2) * chi * N ** 4 + n_out * N * N)
 
 

@@ -61,7 +61,7 @@ struct SweepParams {
     const double2* ovec;     // n_out*N2: ovec[k][i*N+j] = O_k[j][i]  => <O_k> = sum_a ovec[k][a] r[a]
     const int* blk_traj;     // n_blocks*BT trajectory ids (-1: empty slot)
     const int* blk_end;      // n_blocks: last step of the block (max out_end)
-    const int* blk_sys;      // n_blocks: system of the block (all its trajectories share it)
+    const int* blk_sys;      // n_blocks: system of the block's first trajectory (waves index traj_sys)
     const int* traj_sys;     // n_traj: system of each trajectory (chi = 1 kernel)
     long long m_stride;      // complex elements between the free propagators of consecutive systems
     const int* wbeg;         // per trajectory

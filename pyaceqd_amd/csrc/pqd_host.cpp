@@ -476,7 +476,8 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     HIPCHK(P->woff.upload(reinterpret_cast<const long long*>(tr->out_offset), std::max(1, tr->n_traj), s));
     std::vector<int> order(tr->n_traj);
     for (int t = 0; t < tr->n_traj; ++t) order[t] = t;
-    // group by system (a workgroup shares one set of free propagators), longest first inside a system
+    // group by system (a workgroup whose trajectories share one system reads one set of free propagators),
+    // longest first inside a system
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
         if (tsys[a] != tsys[b]) return tsys[a] < tsys[b];
         return tr->out_end[a] > tr->out_end[b];
@@ -493,10 +494,12 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     if (P->CHI > 64) BT = 4;  // chi = 128: only four augmented states fit the LDS
     P->BT = BT;
     std::vector<int> bt, be, bs;
-    for (size_t k = 0; k < order.size();) {  // blocks never mix systems
+    // blocks are filled in this order and may straddle systems (each wave indexes its own system's propagators),
+    // so a scan with one trajectory per system still fills every slot of a workgroup
+    for (size_t k = 0; k < order.size();) {
         const int sy = tsys[order[k]];
         int filled = 0, end = 0;
-        while (k < order.size() && filled < BT && tsys[order[k]] == sy) {
+        while (k < order.size() && filled < BT) {
             bt.push_back(order[k]);
             end = std::max(end, tr->out_end[order[k]]);
             ++k; ++filled;

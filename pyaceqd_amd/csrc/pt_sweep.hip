@@ -314,7 +314,7 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
     extern __shared__ __attribute__((aligned(16))) double2 smem[];
     double2* st = smem;
     double2* rbuf = smem + BT * TS;
-    __shared__ int s_traj[BT], s_wb[BT], s_we[BT], s_fz[BT];
+    __shared__ int s_traj[BT], s_wb[BT], s_we[BT], s_fz[BT], s_sys[BT];
     __shared__ long long s_wo[BT];
 
     const int tid = threadIdx.x;
@@ -328,12 +328,17 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
         s_we[tid] = t >= 0 ? p.wend[t] : -1;
         s_wo[tid] = t >= 0 ? p.woff[t] : 0;
         s_fz[tid] = 0;
+        s_sys[tid] = t >= 0 ? p.traj_sys[t] : 0;
     }
     __syncthreads();
     const int n_end = p.blk_end[blockIdx.x];
-    Mg += (size_t)p.blk_sys[blockIdx.x] * p.m_stride;
-    Fg += (size_t)p.blk_sys[blockIdx.x] * p.f_stride;
-    Wg += (size_t)p.blk_sys[blockIdx.x] * p.w_stride;
+    // a workgroup may mix systems (per-trajectory drives, e.g. one system per scan point): each wave reads the
+    // free propagators of its own trajectory's system
+    {
+        const int sw = __builtin_amdgcn_readfirstlane(s_sys[wave]);
+        Mg += (size_t)sw * p.m_stride;
+        Fg += (size_t)sw * p.f_stride;
+    }
 
     // ---- initial augmented states rho0 (x) bond0 (thread -> column)
     for (int c = tid; c < NCOL; c += NT) {
@@ -393,7 +398,8 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
                 if (s_wb[b] <= n && n <= s_we[b]) {
                     double2 s = c_zero();
                     // fused trajectories still hold the state before M_b(n-1): read it through W(n)
-                    const double2* ov = (s_fz[b] ? Wg + (size_t)n * p.n_out * N2 : p.ovec) + (size_t)k * N2;
+                    const double2* ov = (s_fz[b] ? Wg + (size_t)s_sys[b] * p.w_stride + (size_t)n * p.n_out * N2
+                                                 : p.ovec) + (size_t)k * N2;
                     for (int a = 0; a < N2; ++a) c_fma(s, ov[a], rbuf[b * N2 + a]);
                     outg[s_wo[b] + (long long)(n - s_wb[b]) * p.n_out + k] = s;
                 }

@@ -1,0 +1,137 @@
+"""Throughput of the PT sweep on the other SURVEY.md §8d configurations (bench.py measures the C3/C4 metric line).
+
+One JSON line per config: executed traj-steps/s, pt_sweep ms per launch (HIP events) and TFLOP/s in SURVEY §8d's
+algorithmic flops (fused half steps: F = 8 (D chi^2 + chi N^4 + n_out N^2), D = N^2, no dictionary).
+  c1      TLS, N=2, no PT (chi=1), 1,000 steps: a pulse-area scan of 4096 trajectories
+  c2      TLS, N=2, synthetic chi=32 PT, 10,000 steps, 2048 trajectories (area scan)
+  c3one   biexciton, N=4, chi=64, 10,000 steps, ONE trajectory (the reference's single-run case: latency)
+  c5      six-level linear model, N=6, chi=64, 32 scan points x 64 t1 points = 2048 trajectories, 2,000 tau steps
+usage: python scripts/bench_configs.py [--configs c1,c2,c3one,c5] [--steps 3]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, HERE)
+
+PEAK = 78.6
+
+
+def _xy(p, t):
+    if hasattr(p, "get_total_xy"):
+        return p.get_total_xy(t)
+    f = p.get_total(t)
+    return p.polar_x * f, p.polar_y * f
+
+
+def workload(model, n_scan, n_t1, n_tau, chi, dt=0.1):
+    from pyaceqd_amd import engine, opgrammar, pt as ptmod
+    from pyaceqd_amd.constants import hbar
+    from pyaceqd_amd.pulses import ChirpedPulse, PulseTrain
+    if model == "tls":
+        N = 2  # tls.py:24-29 strings
+        so, bo, lo, io = [], "1.000*|1><1|_2", [["|0><1|_2", 1 / 100]], [["|1><0|_2", "x"]]
+        A, B, C = "|1><0|_2", "|1><1|_2", "|0><1|_2"
+        mk = lambda e0: ChirpedPulse(tau_0=3, e_start=0, e0=e0, t0=20)  # noqa: E731
+    elif model == "biexciton":
+        from pyaceqd_amd.four_level_system.linear import biexciton_ops
+        N = 4
+        so, bo, lo, io, _ = biexciton_ops(delta_b=4, lindblad=True)
+        A, B, C = "|3><1|_4", "|1><1|_4", "|1><3|_4"
+        mk = lambda e0: PulseTrain(100, 10, ChirpedPulse(tau_0=3, e_start=-2.0, e0=e0, t0=12, polar_x=1.0))  # noqa
+    else:
+        from pyaceqd_amd.six_level_system.linear import energies_linear, sixls_ops
+        N = 6
+        so, bo, lo, io, _ = sixls_ops(delta_b=4, lindblad=True, bx=1.0)
+        E_X, _, _, _, E_B = energies_linear(delta_B=4)
+        A, B, C = "|5><1|_6", "|1><1|_6", "|1><5|_6"
+
+        class _Two:  # tests/six_level_linear.py:6-8 pulse pair, e0 of the first pulse scanned
+            def __init__(self, e0):
+                self.p = [ChirpedPulse(tau_0=2.7, e_start=E_X, alpha=40, e0=e0),
+                          ChirpedPulse(tau_0=2.7, e_start=E_B - E_X, alpha=40, e0=4.06, t0=120)]
+
+            def get_total_xy(self, t):
+                xs = [_xy(p, t) for p in self.p]
+                return sum(x for x, _ in xs), sum(y for _, y in xs)
+        mk = _Two
+    mat = lambda s: opgrammar.to_matrix(s, N)  # noqa: E731
+    n_steps = (n_t1 - 1) + n_tau
+    ds = dt / 4
+    ts = ds * np.arange(4 * n_steps + 1)
+    H0 = sum((mat(s) for s in so), np.zeros((N, N), complex))
+    lind = [(r, mat(o)) for o, r in lo if r != 0]
+    systems = []
+    for k in range(n_scan):
+        fx, fy = _xy(mk(1.0 + 5.0 * k / max(1, n_scan)), ts)
+        chans = [(-0.5 * np.pi * hbar * mat(op), fx if pol == "x" else fy) for op, pol in io]
+        systems.append(engine.System(dim=N, H0=H0, lindblad=lind, channels=chans, sample_t0=0.0, sample_dt=ds))
+    grid = engine.Grid(0.0, dt, n_steps, 1)
+    pt = None
+    if chi > 1:
+        pt = ptmod.synthetic_pt(mat(bo), chi=chi, n_init=min(410, n_steps), n_rep=1, seed=1234, eps=0.05, dt=dt)
+    mtos, beg, end, sysidx = [], [], [], []
+    for k in range(n_scan):
+        for t1 in range(n_t1):
+            t = len(beg)
+            if n_t1 > 1:
+                mtos.append(engine.MTO(t, t1, False, 2, mat(A)))
+                mtos.append(engine.MTO(t, t1, False, 1, mat(C)))
+            beg.append(t1 if n_t1 > 1 else 0)
+            end.append(t1 + n_tau)
+            sysidx.append(k)
+    tr = engine.Trajectories(np.array(beg), np.array(end), mtos, system=np.array(sysidx))
+    ops = [mat(B), mat(A) @ mat(B) @ mat(C)]
+    rho0 = mat("|0><0|_%d" % N)
+    return N, (systems if n_scan > 1 else systems[0]), grid, pt, rho0, ops, tr
+
+
+CONFIGS = {
+    "c1": dict(model="tls", n_scan=4096, n_t1=1, n_tau=1000, chi=1),
+    "c2": dict(model="tls", n_scan=2048, n_t1=1, n_tau=10000, chi=32),
+    "c3one": dict(model="biexciton", n_scan=1, n_t1=1, n_tau=10000, chi=64),
+    "c5": dict(model="sixls", n_scan=32, n_t1=64, n_tau=2000, chi=64),
+}
+
+
+def run(name, steps):
+    from pyaceqd_amd import engine
+    cfg = CONFIGS[name]
+    N, sysd, grid, pt, rho0, ops, tr = workload(**cfg)
+    plan = engine.Plan(sysd, grid, rho0, ops, tr, pt=pt)
+    plan.execute()
+    plan.synchronize()
+    plan.timing(reset=True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        plan.execute()
+    plan.synchronize()
+    el = (time.perf_counter() - t0) / steps
+    ms_free, ms_sweep, _ = plan.timing(reset=True)
+    res = plan.download()
+    assert all(np.all(np.isfinite(r)) for r in res), "non-finite output"
+    executed = int(np.sum(tr.out_end + 1))
+    chi = cfg["chi"]
+    F = 8 * (N * N * chi * chi + chi * N ** 4 + len(ops) * N * N) if chi > 1 else 8 * (N ** 4 + len(ops) * N * N)
+    tf = executed * F / (ms_sweep * 1e-3) / 1e12
+    return {"config": name, **cfg, "N": N, "n_traj": tr.n_traj, "executed_traj_steps": executed,
+            "wall_ms_per_launch": el * 1e3, "pt_sweep_ms": ms_sweep, "free_prop_ms": ms_free,
+            "traj_steps_per_s": executed / el, "flop_per_traj_step": F, "sweep_TFLOPs": tf, "frac_fp64": tf / PEAK}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="c1,c2,c3one,c5")
+    ap.add_argument("--steps", type=int, default=3)
+    args = ap.parse_args()
+    for name in args.configs.split(","):
+        print(json.dumps(run(name, args.steps)), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -22,10 +22,23 @@ def main():
     ap.add_argument("--variants", default="0,1,2,4,3,5,6,7")
     ap.add_argument("--pt-modes", default="1", help="PQD_PT_MODE values to cross with the ablations")
     ap.add_argument("--fuse-modes", default="1", help="PQD_FUSE values to cross with the ablations")
+    ap.add_argument("--config", default=None, help="a scripts/bench_configs.py config instead of the bench workload")
+    ap.add_argument("--scan", type=int, default=None, help="with --config: override its scan points")
     args = ap.parse_args()
     import bench
     from pyaceqd_amd import engine
-    sysd, grid, pt, rho0, ops, tr = bench.build_workload(args.traj, args.n_tau, args.chi)
+    N = 4
+    if args.config:
+        sys.path.insert(0, os.path.join(HERE, "scripts"))
+        import bench_configs
+        cfg = dict(bench_configs.CONFIGS[args.config], n_tau=args.n_tau)
+        if args.scan:
+            cfg["n_scan"] = args.scan
+        args.chi = cfg["chi"]
+        N, sysd, grid, pt, rho0, ops, tr = bench_configs.workload(**cfg)
+        args.traj = tr.n_traj
+    else:
+        sysd, grid, pt, rho0, ops, tr = bench.build_workload(args.traj, args.n_tau, args.chi)
     plans = {}
     for fm in [int(x) for x in args.fuse_modes.split(",")]:
         for pm in [int(x) for x in args.pt_modes.split(",")]:
@@ -48,7 +61,7 @@ def main():
             f, w, n = p.timing(reset=True)
             res[v].append(w)
     executed = int(sum(tr.out_end + 1))
-    F = bench.flops_per_traj_step(4, args.chi, len(ops), fused=False)  # full-work equivalent (unfused)
+    F = bench.flops_per_traj_step(N, args.chi, len(ops), fused=False)  # full-work equivalent (unfused)
     out = {}
     for v, ws in res.items():
         ms = min(ws)

@@ -320,13 +320,19 @@ def test_sweep_pt_bt8(monkeypatch, N, chi):
               oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
 
 
+@pytest.mark.parametrize("fuse", ["0", "1"])
+@pytest.mark.parametrize("bt", ["4", "8"])
 @pytest.mark.parametrize("with_pt", [False, True])
-def test_multi_system_scan(with_pt):
+def test_multi_system_scan(monkeypatch, with_pt, bt, fuse):
+    """trajectories of several systems; workgroups straddle systems (each wave reads its own system's free
+    propagators and fused output maps)"""
+    monkeypatch.setenv("PQD_BT", bt)
+    monkeypatch.setenv("PQD_FUSE", fuse)
     N = 4
-    systems = [H.random_system(N, n_steps=30, seed=20 + k)[0] for k in range(3)]
+    systems = [H.random_system(N, n_steps=30, seed=20 + k)[0] for k in range(5)]
     grid = Grid(0.0, 0.1, 30)
-    tr = _traj(grid.n_steps, N, 13, seed=9)
-    tr.system = np.array([k % 3 for k in range(13)])
+    tr = _traj(grid.n_steps, N, 21, seed=9)
+    tr.system = np.array([k % 5 for k in range(21)])
     pt = ptmod.random_pt(N, 32, D=9, n_slices=5, seed=3, eps=0.1) if with_pt else None
     ops = [H.ketbra(N, 1, 1), H.ketbra(N, 3, 0)]
     rho0 = H.random_rho(N)
