@@ -30,7 +30,7 @@ PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 (vector == matrix on gfx950), spec
 PEAK_HBM_GBS = 8000.0
 
 
-def build_workload(n_t1, n_tau, chi, scan=1, scan_offset=0, dt=0.1, seed=1234):
+def build_workload(n_t1, n_tau, chi, scan=1, scan_offset=0, dt=0.1, seed=1234, dictionary=False):
     """(systems, grid, pt, rho0, ops, traj): `scan` pulse-area points x `n_t1` t1 points"""
     from pyaceqd_amd import engine, opgrammar, pt as ptmod
     from pyaceqd_amd.constants import hbar
@@ -53,7 +53,8 @@ def build_workload(n_t1, n_tau, chi, scan=1, scan_offset=0, dt=0.1, seed=1234):
         chans = [(-0.5 * np.pi * hbar * mat(op), fx if pol == "x" else fy) for op, pol in io]
         systems.append(engine.System(dim=N, H0=H0, lindblad=lind, channels=chans, sample_t0=0.0, sample_dt=ds))
     grid = engine.Grid(0.0, dt, n_steps, 1)
-    pt = ptmod.synthetic_pt(mat(bo), chi=chi, n_init=min(410, n_steps), n_rep=1, seed=seed, eps=0.05, dt=dt)
+    pt = ptmod.synthetic_pt(mat(bo), chi=chi, n_init=min(410, n_steps), n_rep=1, seed=seed, eps=0.05, dt=dt,
+                            dictionary=dictionary)
     A, B, Cm = mat("|3><1|_4"), mat("|1><1|_4"), mat("|1><3|_4")
     mtos, beg, end, sysidx = [], [], [], []
     for k in range(scan):
@@ -134,6 +135,8 @@ def main():
     ap.add_argument("--scan", type=int, default=8, help="pulse-area scan points per GPU")
     ap.add_argument("--n-tau", type=int, default=10000)
     ap.add_argument("--chi", type=int, default=64)
+    ap.add_argument("--pt-dict", type=int, default=0,
+                    help="1: dictionary PT (9 slices for the 16 rows, as generated physical PTs have); 0: 16 slices")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
@@ -154,7 +157,7 @@ def main():
     from pyaceqd_amd import _lib, engine
     ctx = _lib.context(local)
     sysd, grid, pt, rho0, ops, tr = build_workload(args.t1, args.n_tau, args.chi, scan=args.scan,
-                                                   scan_offset=rank * args.scan)
+                                                   scan_offset=rank * args.scan, dictionary=bool(args.pt_dict))
     n_traj = tr.n_traj
     plan = engine.Plan(sysd, grid, rho0, ops, tr, pt=pt, ctx=ctx)
 

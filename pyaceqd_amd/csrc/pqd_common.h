@@ -78,6 +78,8 @@ struct SweepParams {
     int pt_mode;             // PT contraction: 0 VALU, 1 matrix cores (4x4x4_4b), 2 mixed per wave,
                              //   3 split-complex 16x16x4 (BT = 8), 4 matrix cores with 3 real products (3M)
     int cmul3;               // column phases with 3 real products per complex product (3M)
+    const int4* units;       // 3M PT rows per wave: [BT][umax] (slice, row, row sharing the slice or -1, 0),
+    int umax;                //   a unit with slice < 0 ends a wave's list; NULL: rows a = wave + k BT
     int ablate;              // diagnostics only (PQD_ABLATE): 1 skip PT, 2 skip column phases, 4 skip outputs
 };
 

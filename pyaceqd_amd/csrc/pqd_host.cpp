@@ -197,6 +197,7 @@ struct pqd_pt {
     int dim = 0, chi = 0, CHI = 0, D = 0, n_slices = 0;
     DevBuf<double2> Q, closure, closure0, bond0;
     DevBuf<int> gmap;
+    std::vector<int> gmap_h;  // host copy: the plan derives its PT row units from it
 };
 
 struct pqd_plan {
@@ -208,7 +209,7 @@ struct pqd_plan {
     FuseParams fu{};
     DevBuf<int> sched, blk_traj, blk_end, blk_sys, traj_sys, wbeg, wend, ev_start;
     DevBuf<long long> woff;
-    DevBuf<int4> ev;
+    DevBuf<int4> ev, units;
     FreePropParams fp{};
     SweepParams sp{};
     int64_t out_len = 0;
@@ -323,6 +324,7 @@ int pqd_pt_create(pqd_ctx* ctx, int32_t dim, const pqd_pt_desc* d, pqd_pt** out)
     std::memcpy(b0.data(), d->bond0, sizeof(double2) * chi);
     auto* pt = new pqd_pt;
     pt->ctx = ctx; pt->dim = dim; pt->chi = chi; pt->CHI = CHI; pt->D = d->D; pt->n_slices = d->n_slices;
+    pt->gmap_h.assign(d->gmap, d->gmap + N2);
     hipError_t e = pt->Q.upload(Q.data(), qn, ctx->stream);
     if (e == hipSuccess) e = pt->closure.upload(cl.data(), cl.size(), ctx->stream);
     if (e == hipSuccess) e = pt->closure0.upload(c0.data(), CHI, ctx->stream);
@@ -359,6 +361,40 @@ int pqd_free_propagators(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* gr
     if (nM) HIPCHK(hipMemcpyAsync(M_out, M.p, nM * sizeof(double2), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     return PQD_OK;
+}
+
+// PT rows per wave for the 3M sweep. Rows whose coupling-eigenvalue pair maps to the same slice (dictionary
+// PTs, e.g. 16 biexciton rows over 9 slices) are paired, so one L2 read of a slice feeds two rows. Units
+// (pair cost 2, single cost 1) go to the least-loaded wave, longest first. Each wave's list ends with slice -1.
+static std::vector<int4> pt_row_units(const std::vector<int>& gmap, int NW, int pair) {
+    const int N2 = (int)gmap.size();
+    std::vector<int4> units;
+    std::vector<int> done(N2, 0);
+    for (int a = 0; a < N2; ++a) {
+        if (done[a]) continue;
+        done[a] = 1;
+        int b = -1;
+        if (pair)
+            for (int c = a + 1; c < N2; ++c)
+                if (!done[c] && gmap[c] == gmap[a]) { b = c; done[c] = 1; break; }
+        units.push_back(make_int4(gmap[a], a, b, 0));
+    }
+    std::stable_sort(units.begin(), units.end(), [](const int4& x, const int4& y) { return (x.z >= 0) > (y.z >= 0); });
+    std::vector<std::vector<int4>> per(NW);
+    std::vector<int> load(NW, 0);
+    for (const int4& e : units) {
+        int w = 0;
+        for (int k = 1; k < NW; ++k)
+            if (load[k] < load[w]) w = k;
+        per[w].push_back(e);
+        load[w] += e.z >= 0 ? 2 : 1;
+    }
+    size_t umax = 1;
+    for (auto& v : per) umax = std::max(umax, v.size() + 1);
+    std::vector<int4> out((size_t)NW * umax, make_int4(-1, -1, -1, 0));
+    for (int w = 0; w < NW; ++w)
+        for (size_t k = 0; k < per[w].size(); ++k) out[(size_t)w * umax + k] = per[w][k];
+    return out;
 }
 
 int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems, const int32_t* traj_sys,
@@ -533,6 +569,12 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     { const char* ab = getenv("PQD_ABLATE"); sp.ablate = ab ? atoi(ab) : 0; }
     { const char* pm = getenv("PQD_PT_MODE"); sp.pt_mode = pm ? atoi(pm) : 4; }
     { const char* c3 = getenv("PQD_CMUL3"); sp.cmul3 = c3 ? atoi(c3) : 1; }
+    if (pt && (sp.pt_mode == 4 || sp.pt_mode == 5)) {
+        std::vector<int4> u = pt_row_units(pt->gmap_h, P->BT, getenv("PQD_ROWPAIR") ? atoi(getenv("PQD_ROWPAIR")) : 1);
+        HIPCHK(P->units.upload(u.data(), u.size(), s));
+        sp.units = P->units.p;
+        sp.umax = (int)(u.size() / P->BT);
+    }
     { const char* fz = getenv("PQD_FUSE"); sp.fuse = (!P->nopt && ns > 0 && (fz ? atoi(fz) : 1)) ? 1 : 0; }
     if (sp.fuse) {
         HIPCHK(P->F.alloc((size_t)n_sys * ns * m2));

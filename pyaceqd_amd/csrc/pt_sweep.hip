@@ -211,16 +211,23 @@ __device__ __forceinline__ void pt_row_mfma(const double2* __restrict__ Qg, doub
 // pt_row_mfma with three real products per complex product (3M, see col_apply_mfma3): 3 MFMA chains per
 // (row block, column group) instead of 4; (Qr + Qi) and (Xr + Xi) are one VALU add per loaded element.
 // PF = how many k-steps of the PT slice are in flight ahead of the MFMAs (L2 latency hiding).
-template <int CHI, int BT, int RS, int TS, int PF = 1>
-__device__ __forceinline__ void pt_row_mfma3(const double2* __restrict__ Qg, double2* st, int a, int lane) {
+// R = 2 contracts two Liouville rows a0, a1 that share one PT slice (dictionary PTs: rows with the same
+// coupling-eigenvalue pair) in one pass, so each slice element loaded from L2 feeds twice the MFMAs.
+template <int CHI, int BT, int RS, int TS, int PF = 1, int R = 1>
+__device__ __forceinline__ void pt_row_mfma3(const double2* __restrict__ Qg, double2* st, int a0, int a1,
+                                             int lane) {
     constexpr int RB = BT / 4, NG = CHI / 16, KSN = CHI / 4;
     const int x = lane & 3, kk = lane >> 4, c16 = lane & 15;
-    double p1[RB][NG], p2[RB][NG], p3[RB][NG];
+    double p1[R][RB][NG], p2[R][RB][NG], p3[R][RB][NG];
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb)
+    for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int g = 0; g < NG; ++g) { p1[rb][g] = 0.0; p2[rb][g] = 0.0; p3[rb][g] = 0.0; }
-    const double2* xr = st + a * RS + kk;
+        for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+            for (int g = 0; g < NG; ++g) { p1[r][rb][g] = 0.0; p2[r][rb][g] = 0.0; p3[r][rb][g] = 0.0; }
+    const double2* xr[R];
+    xr[0] = st + a0 * RS + kk;
+    if constexpr (R == 2) xr[R - 1] = st + a1 * RS + kk;
     const double2* qp = Qg + (size_t)kk * CHI + c16;
     double2 qn[PF][NG];
 #pragma unroll
@@ -242,23 +249,29 @@ __device__ __forceinline__ void pt_row_mfma3(const double2* __restrict__ Qg, dou
             for (int g = 0; g < NG; ++g) qn[PF - 1][g] = qp[(size_t)4 * (ks + PF) * CHI + 16 * g];
         }
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb) {
-            const double2 av = xr[(4 * rb + x) * TS + 4 * ks];
-            const double as = av.x + av.y;
+        for (int r = 0; r < R; ++r)
 #pragma unroll
-            for (int g = 0; g < NG; ++g) {
-                p1[rb][g] = __builtin_amdgcn_mfma_f64_4x4x4f64(av.x, qv[g].x, p1[rb][g], 0, 0, 0);
-                p2[rb][g] = __builtin_amdgcn_mfma_f64_4x4x4f64(av.y, qv[g].y, p2[rb][g], 0, 0, 0);
-                p3[rb][g] = __builtin_amdgcn_mfma_f64_4x4x4f64(as, qs[g], p3[rb][g], 0, 0, 0);
+            for (int rb = 0; rb < RB; ++rb) {
+                const double2 av = xr[r][(4 * rb + x) * TS + 4 * ks];
+                const double as = av.x + av.y;
+#pragma unroll
+                for (int g = 0; g < NG; ++g) {
+                    p1[r][rb][g] = __builtin_amdgcn_mfma_f64_4x4x4f64(av.x, qv[g].x, p1[r][rb][g], 0, 0, 0);
+                    p2[r][rb][g] = __builtin_amdgcn_mfma_f64_4x4x4f64(av.y, qv[g].y, p2[r][rb][g], 0, 0, 0);
+                    p3[r][rb][g] = __builtin_amdgcn_mfma_f64_4x4x4f64(as, qs[g], p3[r][rb][g], 0, 0, 0);
+                }
             }
-        }
     }
-    double2* wr = st + a * RS + c16;
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb)
+    for (int r = 0; r < R; ++r) {
+        double2* wr = st + (r == 0 ? a0 : a1) * RS + c16;
 #pragma unroll
-        for (int g = 0; g < NG; ++g)
-            wr[(4 * rb + kk) * TS + 16 * g] = make_double2(p1[rb][g] - p2[rb][g], p3[rb][g] - p1[rb][g] - p2[rb][g]);
+        for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+            for (int g = 0; g < NG; ++g)
+                wr[(4 * rb + kk) * TS + 16 * g] = make_double2(p1[r][rb][g] - p2[r][rb][g],
+                                                               p3[r][rb][g] - p1[r][rb][g] - p2[r][rb][g]);
+    }
 }
 
 // PT contraction of row alpha for BT = 8 on v_mfma_f64_16x16x4_f64 ("split complex"): the 16 MFMA rows are
@@ -431,16 +444,32 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
             // complex product (default), 3: split-complex 16x16x4 rows (BT = 8), 2: mixed (waves 0..NW/2-1 start on the matrix cores,
             // the others on the VALU, alternating per row), so the two FP64 pipes of a SIMD run concurrently
             int parity = (p.pt_mode == 2) ? ((wave >= NW / 2) ? 1 : 0) : 0;
+            if (p.units && (p.pt_mode == 4 || p.pt_mode == 5)) {
+                // 3M rows by the host's per-wave unit list: (slice, row, second row sharing the slice or -1)
+                const int4* U = p.units + (size_t)wave * p.umax;
+                for (int u = 0; u < p.umax; ++u) {
+                    const int4 e = U[u];
+                    if (e.x < 0) break;
+                    const double2* Qg = Qs + (size_t)e.x * CHI * CHI;
+                    if (p.pt_mode == 5) {
+                        if (e.z >= 0) pt_row_mfma3<CHI, BT, RS, TS, 2, 2>(Qg, st, e.y, e.z, lane);
+                        else pt_row_mfma3<CHI, BT, RS, TS, 2, 1>(Qg, st, e.y, e.y, lane);
+                    } else {
+                        if (e.z >= 0) pt_row_mfma3<CHI, BT, RS, TS, 1, 2>(Qg, st, e.y, e.z, lane);
+                        else pt_row_mfma3<CHI, BT, RS, TS, 1, 1>(Qg, st, e.y, e.y, lane);
+                    }
+                }
+            } else
             for (int a = wave; a < N2; a += NW) {
                 const double2* Qg = Qs + (size_t)p.gmap[a] * CHI * CHI;
                 const bool use_mfma = (p.pt_mode == 1) || (p.pt_mode == 2 && parity == 0);
                 parity ^= 1;
                 if (p.pt_mode == 4) {
-                    pt_row_mfma3<CHI, BT, RS, TS, 1>(Qg, st, a, lane);
+                    pt_row_mfma3<CHI, BT, RS, TS, 1>(Qg, st, a, a, lane);
                     continue;
                 }
                 if (p.pt_mode == 5) {   // 3M with two k-steps of the slice in flight
-                    pt_row_mfma3<CHI, BT, RS, TS, 2>(Qg, st, a, lane);
+                    pt_row_mfma3<CHI, BT, RS, TS, 2>(Qg, st, a, a, lane);
                     continue;
                 }
                 if constexpr (BT == 8) {

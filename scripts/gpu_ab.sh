@@ -8,7 +8,8 @@ while IFS= read -r v; do
   [ -z "$v" ] && continue
   i=$((i+1))
   echo "== variant $i: $v"
-  env $v timeout -k 10 300 python bench.py --steps ${BENCH_STEPS:-3} --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/ab_$i.log 2>&1
+  ve=${v%%|*}; va=""; [[ $v == *"|"* ]] && va=${v#*|}   # "ENV=.. ENV=.. | bench args"
+  env $ve timeout -k 10 300 python bench.py --steps ${BENCH_STEPS:-3} --warmup 1 --no-cpu-baseline ${BENCH_ARGS} $va > gpurun_out/ab_$i.log 2>&1
   rc=$?; echo "rc=$rc"; grep -o '"value": [0-9.e+]*\|"pt_sweep": [0-9.]*\|"frac": [0-9.]*' gpurun_out/ab_$i.log | tr '\n' ' '; echo
   if crash $rc; then tail -20 gpurun_out/ab_$i.log; exit $rc; fi
 done <<< "${VARIANTS:-PQD_PT_MODE=4 PQD_CMUL3=1
