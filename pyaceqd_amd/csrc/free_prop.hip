@@ -6,8 +6,9 @@
 // All trajectories at the same absolute step share these matrices, so they are built once per
 // step here (2 * n_steps independent N2 x N2 expm's: 16x16 at N=4, 36x36 at N=6).
 //
-// Algorithm per matrix (same as the oracle's or_expm): A = L(t) w, s = max(0, e) with
-// frexp(||A||_1 / 0.5) = m 2^e, degree-18 Taylor polynomial by Horner on A 2^-s, then s squarings.
+// Algorithm per matrix (the oracle's or_expm, with the degree cut to the precision): A = L(t) w,
+// s = max(0, e) with frexp(||A||_1 / 0.5) = m 2^e, Taylor polynomial by Horner on A 2^-s of the smallest
+// degree <= 18 whose remainder bound is below 2^-56 (the oracle always uses 18), then s squarings.
 // The N2 x N2 operands live in LDS; each of the 256 threads owns ceil(N2^2/256) output entries.
 #include "pqd_common.h"
 
@@ -44,7 +45,7 @@ __global__ __launch_bounds__(256) void free_prop_kernel(FreePropParams p) {
     double2* T = P + N2 * N2;
     double2* Acc = T + N2 * N2;
     __shared__ double colsum[N2];
-    __shared__ int s_sh;
+    __shared__ int s_sh, s_deg;
 
     const int tid = threadIdx.x;
     const int si = blockIdx.x / (2 * p.n_steps);
@@ -81,21 +82,30 @@ __global__ __launch_bounds__(256) void free_prop_kernel(FreePropParams p) {
             for (int c = 0; c < N2; ++c) norm = colsum[c] > norm ? colsum[c] : norm;
             int e2 = 0;
             frexp(norm / 0.5, &e2);
-            s_sh = e2 > 0 ? e2 : 0;
+            const int s = e2 > 0 ? e2 : 0;
+            // Taylor degree: the smallest m <= 18 whose remainder bound theta^(m+1)/(m+1)! e^theta on the
+            // scaled matrix (theta <= 0.5) is below 2^-56, so the series stops at double precision instead of
+            // always running 18 terms (theta = 0.5 needs 15 terms, smaller norms fewer)
+            const double theta = ldexp(norm, -s);
+            double rem = 0.5 * theta * theta;  // theta^(deg+1)/(deg+1)! for deg = 1
+            int deg = 1;
+            while (deg < 18 && rem * 1.7 > 1.4e-17) { ++deg; rem *= theta / (deg + 1); }
+            s_sh = s;
+            s_deg = deg;
         }
         __syncthreads();
-        const int s = s_sh;
+        const int s = s_sh, deg = s_deg;
         const double scale = ldexp(1.0, -s);
         for (int e = tid; e < N2 * N2; e += 256) {
             const double2 a = c_scale(A[e], scale);
             A[e] = a;
-            double2 pv = make_double2(a.x / 18.0, a.y / 18.0);
+            double2 pv = make_double2(a.x / (double)deg, a.y / (double)deg);
             const int i = e / N2;
             if (e == i * N2 + i) pv.x += 1.0;
             P[e] = pv;
         }
         __syncthreads();
-        for (int mm = 17; mm >= 1; --mm) {
+        for (int mm = deg - 1; mm >= 1; --mm) {
             lds_matmul<N2>(A, P, T, tid);
             __syncthreads();
             for (int e = tid; e < N2 * N2; e += 256) {

@@ -126,6 +126,9 @@ struct FuseParams {          // F(m) = M_a(m) M_b(m-1) (1 <= m < n_steps), W(m) 
 
 hipError_t launch_free_prop(int N2, const FreePropParams& p, hipStream_t s);
 hipError_t launch_fuse_steps(int N2, const FuseParams& p, hipStream_t s);
+// waves per trajectory in the PT sweep: a 4-trajectory workgroup (N2 > 16 or chi = 128) runs 8 waves, two per
+// trajectory (each owns half of the bond columns in the column phases), so every SIMD holds two waves
+constexpr int sweep_wpt(int BT, int CHI) { return (BT == 4 && CHI >= 32) ? 2 : 1; }
 hipError_t launch_sweep(int N2, int CHI, int BT, int n_blocks, const SweepParams& p, hipStream_t s);
 int sweep_max_bt(int N2);
 hipError_t launch_sweep_nopt(int N2, int n_blocks, const SweepParams& p, hipStream_t s);

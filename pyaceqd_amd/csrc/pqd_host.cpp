@@ -570,10 +570,11 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     { const char* pm = getenv("PQD_PT_MODE"); sp.pt_mode = pm ? atoi(pm) : 4; }
     { const char* c3 = getenv("PQD_CMUL3"); sp.cmul3 = c3 ? atoi(c3) : 1; }
     if (pt && (sp.pt_mode == 4 || sp.pt_mode == 5)) {
-        std::vector<int4> u = pt_row_units(pt->gmap_h, P->BT, getenv("PQD_ROWPAIR") ? atoi(getenv("PQD_ROWPAIR")) : 1);
+        const int nw = P->BT * sweep_wpt(P->BT, P->CHI);
+        std::vector<int4> u = pt_row_units(pt->gmap_h, nw, getenv("PQD_ROWPAIR") ? atoi(getenv("PQD_ROWPAIR")) : 1);
         HIPCHK(P->units.upload(u.data(), u.size(), s));
         sp.units = P->units.p;
-        sp.umax = (int)(u.size() / P->BT);
+        sp.umax = (int)(u.size() / nw);
     }
     { const char* fz = getenv("PQD_FUSE"); sp.fuse = (!P->nopt && ns > 0 && (fz ? atoi(fz) : 1)) ? 1 : 0; }
     if (sp.fuse) {

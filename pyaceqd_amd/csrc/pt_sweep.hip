@@ -6,21 +6,21 @@
 // two-time sweeps (two_time/correlations.py:135-184, pol_entanglement/G2.py:439-533, ...).
 //
 // Work decomposition (MI355X: 256 CUs, 160 KiB LDS/CU, 64-wide waves, FP64 VALU = FP64 MFMA peak):
-//   * one 256-thread workgroup owns B = 4 trajectories for the whole time range (persistent over
-//     steps, no inter-workgroup traffic at all: trajectories are independent);
-//   * the 4 augmented states Q_b[alpha][d] (N2 x CHI complex doubles, 16 KiB each at N=4, chi=64)
-//     stay resident in LDS, rows padded to CHI+1 so column reads and row reads are bank-conflict free;
-//   * free half steps (N2 x N2 propagator applied to every bond column): one wave per trajectory runs
-//     the complex GEMM M . Q on the FP64 matrix cores (v_mfma_f64_16x16x4_f64, 4 real MFMAs per
-//     complex tile), no cross-wave traffic, no barrier inside the phase;
-//   * PT contraction (row alpha of all 4 trajectories times the chi x chi slice Q[g(alpha)]): waves
-//     split the alpha rows; lane (j, q) owns output columns {j, j+16, j+32, j+48} and the input
-//     quarter d = 4k + q, so every Q element is read from L2 exactly once per workgroup and feeds
-//     4 trajectories (B) from registers; the 4 quarter partial sums are combined by a 2-stage
-//     reduce-scatter over lanes (xor 16, xor 32);
+//   * one workgroup owns BT trajectories (8 at N2 <= 16, else 4) for the whole time range (persistent over
+//     steps, no inter-workgroup traffic: trajectories are independent); 8 waves per workgroup (one per
+//     trajectory at BT = 8, two per trajectory at BT = 4 and chi >= 32, see sweep_wpt);
+//   * the augmented states Q_b[alpha][d] (N2 x CHI complex doubles, 16 KiB each at N=4, chi=64) stay
+//     resident in LDS, rows padded to CHI+1 so column reads and row reads are bank-conflict free;
+//   * free half steps / MTOs (N2 x N2 operator applied to every bond column): the waves of a trajectory
+//     run the complex GEMM M . Q on the FP64 matrix cores (v_mfma_f64_16x16x4_f64, 3 real MFMAs per complex
+//     tile by default), no cross-wave traffic, no barrier inside the phase; steps without MTOs apply the
+//     fused operator F(n) = M_a(n) M_b(n-1) once;
+//   * PT contraction (row alpha of all BT trajectories times the chi x chi slice Q[g(alpha)]): waves take the
+//     rows (or pairs of rows sharing a dictionary slice) of a host-built unit list; v_mfma_f64_4x4x4_4b with
+//     3 real products per complex product, every slice element read from L2 once per workgroup and step;
 //   * closure + output traces only on steps inside some trajectory's output window.
 // All PT slices / free propagators are shared by every workgroup at the same absolute step, so the
-// dominant traffic is L2/MALL-resident; the kernel is FP64-FMA bound at B = 4.
+// dominant traffic is L2/MALL-resident; the kernel is FP64 matrix-core bound.
 #include "pqd_common.h"
 #include <climits>
 
@@ -32,6 +32,8 @@ struct SweepLayout {
     static constexpr int TS = N2 * RS + 4;      // trajectory stride (+64 B: shifts banks per trajectory)
     static constexpr int KD = CHI / 16;         // PT output columns per lane
     static constexpr int NCOL = BT * CHI;       // column-phase work items
+    static constexpr int WPT = sweep_wpt(BT, CHI);  // waves per trajectory
+    static constexpr int NW = BT * WPT;             // waves per workgroup
     static constexpr size_t LDS = (size_t)(BT * TS + BT * N2) * sizeof(double2);
 };
 
@@ -43,13 +45,15 @@ typedef double dbl4 __attribute__((ext_vector_type(4)));
 // complex = 4 real MFMAs (Cr += Ar Br - Ai Bi, Ci += Ar Bi + Ai Br). Fragment maps (gfx950 f64):
 // A[i = l&15][k = l>>4], B[k = l>>4][j = l&15], C[i = (l>>4) + 4 r][j = l&15].
 // Column tiles are the outer loop, so each 16-column tile is read completely before it is written
-// back in place. Rows/k beyond N2 are zero padding (N2 = 4, 9, 25, 36).
-template <int N2, int CHI, int RS>
-__device__ __forceinline__ void col_apply_mfma(const double2* __restrict__ Op, double2* S, int lane) {
+// back in place. With WPT waves per trajectory, wave `half` takes every WPT-th tile (columns are
+// independent). Rows/k beyond N2 are zero padding (N2 = 4, 9, 25, 36).
+template <int N2, int CHI, int RS, int WPT = 1>
+__device__ __forceinline__ void col_apply_mfma(const double2* __restrict__ Op, double2* S, int lane, int half = 0) {
     constexpr int MT = (N2 + 15) / 16;   // output row tiles
     constexpr int KS = (N2 + 3) / 4;     // k steps
     constexpr int NTL = CHI / 16;        // column tiles
     constexpr bool CACHE_A = KS * MT <= 8;
+    constexpr int KSU = CACHE_A ? KS : 3;   // large N2: bounded unroll keeps the operator loads out of VGPRs
     const int li = lane & 15, lk = lane >> 4;
     double2 ac[CACHE_A ? KS * MT : 1];
     if constexpr (CACHE_A) {
@@ -62,11 +66,12 @@ __device__ __forceinline__ void col_apply_mfma(const double2* __restrict__ Op, d
             }
     }
 #pragma unroll
-    for (int nt = 0; nt < NTL; ++nt) {
+    for (int j = 0; j < NTL / WPT; ++j) {   // this wave's column tiles: half, half + WPT, ...
+        const int nt = j * WPT + half;
         dbl4 cr[MT], ci[MT];
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) { cr[mt] = dbl4{0, 0, 0, 0}; ci[mt] = dbl4{0, 0, 0, 0}; }
-#pragma unroll
+#pragma unroll KSU
         for (int ks = 0; ks < KS; ++ks) {
             const int a = 4 * ks + lk;
             const double2 b = (a < N2) ? S[a * RS + 16 * nt + li] : c_zero();
@@ -101,12 +106,13 @@ __device__ __forceinline__ void col_apply_mfma(const double2* __restrict__ Op, d
 // P3 = (Ar + Ai)(Br + Bi); Cr = P1 - P2, Ci = P3 - P1 - P2. Three MFMA chains instead of four, the sums are
 // two VALU adds per operand fragment. Error bound eps (|Ar||Br| + |Ai||Bi| + |Ar + Ai||Br + Bi|) per product,
 // i.e. the same order as the 4M form for these O(1) propagators.
-template <int N2, int CHI, int RS>
-__device__ __forceinline__ void col_apply_mfma3(const double2* __restrict__ Op, double2* S, int lane) {
+template <int N2, int CHI, int RS, int WPT = 1>
+__device__ __forceinline__ void col_apply_mfma3(const double2* __restrict__ Op, double2* S, int lane, int half = 0) {
     constexpr int MT = (N2 + 15) / 16;
     constexpr int KS = (N2 + 3) / 4;
     constexpr int NTL = CHI / 16;
     constexpr bool CACHE_A = KS * MT <= 8;
+    constexpr int KSU = CACHE_A ? KS : 3;   // large N2: bounded unroll keeps the operator loads out of VGPRs
     const int li = lane & 15, lk = lane >> 4;
     double2 ac[CACHE_A ? KS * MT : 1];
     double as[CACHE_A ? KS * MT : 1];
@@ -121,11 +127,12 @@ __device__ __forceinline__ void col_apply_mfma3(const double2* __restrict__ Op, 
             }
     }
 #pragma unroll
-    for (int nt = 0; nt < NTL; ++nt) {
+    for (int j = 0; j < NTL / WPT; ++j) {   // this wave's column tiles: half, half + WPT, ...
+        const int nt = j * WPT + half;
         dbl4 p1[MT], p2[MT], p3[MT];
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) { p1[mt] = dbl4{0, 0, 0, 0}; p2[mt] = p1[mt]; p3[mt] = p1[mt]; }
-#pragma unroll
+#pragma unroll KSU
         for (int ks = 0; ks < KS; ++ks) {
             const int a = 4 * ks + lk;
             const double2 b = (a < N2) ? S[a * RS + 16 * nt + li] : c_zero();
@@ -318,12 +325,12 @@ __device__ __forceinline__ void pt_row_mfma16(const double2* __restrict__ Qg, do
 }
 
 template <int N2, int CHI, int BT>
-__global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const double2* __restrict__ Mg,
+__global__ __launch_bounds__(64 * BT * sweep_wpt(BT, CHI)) void pt_sweep_kernel(SweepParams p, const double2* __restrict__ Mg,
                                                            const double2* __restrict__ Qg0, double2* __restrict__ outg,
                                                            const double2* __restrict__ Fg, const double2* __restrict__ Wg) {
     using L = SweepLayout<N2, CHI, BT>;
     constexpr int RS = L::RS, TS = L::TS, KD = L::KD, NCOL = L::NCOL;
-    constexpr int NT = 64 * BT, NW = BT;  // threads, waves
+    constexpr int WPT = L::WPT, NW = L::NW, NT = 64 * NW;  // waves per trajectory, waves, threads
     extern __shared__ __attribute__((aligned(16))) double2 smem[];
     double2* st = smem;
     double2* rbuf = smem + BT * TS;
@@ -333,6 +340,7 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tw = wave % BT, half = wave / BT;  // column phases: trajectory of this wave, its column half
 
     if (tid < BT) {
         const int t = p.blk_traj[blockIdx.x * BT + tid];
@@ -348,7 +356,7 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
     // a workgroup may mix systems (per-trajectory drives, e.g. one system per scan point): each wave reads the
     // free propagators of its own trajectory's system
     {
-        const int sw = __builtin_amdgcn_readfirstlane(s_sys[wave]);
+        const int sw = __builtin_amdgcn_readfirstlane(s_sys[tw]);
         Mg += (size_t)sw * p.m_stride;
         Fg += (size_t)sw * p.f_stride;
     }
@@ -361,16 +369,17 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
         for (int a = 0; a < N2; ++a) st[cb * TS + a * RS + cd] = c_mul(p.rho0[a], b0);
     }
     __syncthreads();
-    // ---- column phases: wave w owns trajectory w (its free propagators, its MTO events)
-    double2* stw = st + wave * TS;
+    // ---- column phases: wave w owns trajectory w % BT (its free propagators, its MTO events), and with two
+    // waves per trajectory the column tiles of half w / BT
+    double2* stw = st + tw * TS;
     const bool c3 = p.cmul3 != 0;
     auto col = [&](const double2* __restrict__ Op) {
-        if (c3) col_apply_mfma3<N2, CHI, RS>(Op, stw, lane);
-        else col_apply_mfma<N2, CHI, RS>(Op, stw, lane);
+        if (c3) col_apply_mfma3<N2, CHI, RS, WPT>(Op, stw, lane, half);
+        else col_apply_mfma<N2, CHI, RS, WPT>(Op, stw, lane, half);
     };
     int ev_cur = 0, ev_lim = 0;
     {
-        const int t = s_traj[wave];
+        const int t = s_traj[tw];
         if (t >= 0) { ev_cur = p.ev_start[t]; ev_lim = p.ev_start[t + 1]; }
         while (ev_cur < ev_lim) {  // applyBefore-true MTOs at step 0
             const int4 e = p.ev[ev_cur];
@@ -478,14 +487,14 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
                         continue;
                     }
                 }
-                // the VALU rows are compiled for BT = 4 and chi <= 64 only: at BT = 8 (or chi = 128) their
-                // accumulators cap the whole kernel's VGPR allocation and spill, so those run modes 0/2 on the
-                // 4x4x4 path
-                if (BT == 8 || CHI > 64 || use_mfma || p.pt_mode == 3) {
+                // the VALU rows are compiled for BT = 4, chi <= 64 and one wave per trajectory only: elsewhere
+                // their accumulators cap the whole kernel's VGPR allocation and spill, so those run modes 0/2 on
+                // the 4x4x4 path
+                if (BT == 8 || CHI > 64 || WPT > 1 || use_mfma || p.pt_mode == 3) {
                     pt_row_mfma<CHI, BT, RS, TS>(Qg, st, a, lane);
                     continue;
                 }
-                if constexpr (BT == 4 && CHI <= 64) {
+                if constexpr (BT == 4 && CHI <= 64 && WPT == 1) {
                 Qg += pj;
                 const double2* xr = st + a * RS + pq;
                 double2 acc[BT][KD];
@@ -566,7 +575,7 @@ __global__ __launch_bounds__(64 * BT) void pt_sweep_kernel(SweepParams p, const 
                 ++ev_cur;
             }
         }
-        if (lane == 0) s_fz[wave] = fz ? 1 : 0;
+        if (lane == 0 && half == 0) s_fz[tw] = fz ? 1 : 0;
         __syncthreads();
     }
 }
@@ -645,7 +654,7 @@ hipError_t launch_sw(int n_blocks, const SweepParams& p, hipStream_t s) {
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((pt_sweep_kernel<N2, CHI, BT>), dim3(n_blocks), dim3(64 * BT), L::LDS, s, p, p.M, p.Q, p.out,
+    hipLaunchKernelGGL((pt_sweep_kernel<N2, CHI, BT>), dim3(n_blocks), dim3(64 * L::NW), L::LDS, s, p, p.M, p.Q, p.out,
                        p.F, p.W);
     return hipGetLastError();
 }
