@@ -78,7 +78,8 @@ struct SweepParams {
     int pt_mode;             // PT contraction: 0 VALU, 1 matrix cores (4x4x4_4b), 2 mixed per wave,
                              //   3 split-complex 16x16x4 (BT = 8), 4 matrix cores with 3 real products (3M)
     int cmul3;               // column phases with 3 real products per complex product (3M)
-    const int4* units;       // 3M PT rows per wave: [BT][umax] (slice, row, row sharing the slice or -1, 0),
+    const int4* units;       // 3M PT rows per wave: [waves][umax] (slice, row 0, row 1 or -1, row 2 | row 3 << 16 or -1;
+                             //   a missing row 3 is 0x7FFF),
     int umax;                //   a unit with slice < 0 ends a wave's list; NULL: rows a = wave + k BT
     int ablate;              // diagnostics only (PQD_ABLATE): 1 skip PT, 2 skip column phases, 4 skip outputs
 };
@@ -129,6 +130,13 @@ hipError_t launch_fuse_steps(int N2, const FuseParams& p, hipStream_t s);
 // waves per trajectory in the PT sweep: a 4-trajectory workgroup (N2 > 16 or chi = 128) runs 8 waves, two per
 // trajectory (each owns half of the bond columns in the column phases), so every SIMD holds two waves
 constexpr int sweep_wpt(int BT, int CHI) { return (BT == 4 && CHI >= 32) ? 2 : 1; }
+// rows per PT unit (rows sharing one dictionary slice contracted together): 3 R (BT/4) (CHI/16) accumulators <= 48
+// (quads only at N2 > 16, where the 4-trajectory slice stream is L2-bound; smaller N2 keep pairs)
+constexpr int sweep_rmax(int N2, int BT, int CHI) {
+    const int acc = (BT >= 8 ? BT / 4 : 1) * (CHI >= 16 ? CHI / 16 : 1);  // accumulators per row and product
+    const int r = 16 / acc >= 4 ? 4 : (16 / acc >= 2 ? 2 : 1);
+    return N2 > 16 ? r : (r > 2 ? 2 : r);
+}
 hipError_t launch_sweep(int N2, int CHI, int BT, int n_blocks, const SweepParams& p, hipStream_t s);
 int sweep_max_bt(int N2);
 hipError_t launch_sweep_nopt(int N2, int n_blocks, const SweepParams& p, hipStream_t s);

@@ -364,22 +364,24 @@ int pqd_free_propagators(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* gr
 }
 
 // PT rows per wave for the 3M sweep. Rows whose coupling-eigenvalue pair maps to the same slice (dictionary
-// PTs, e.g. 16 biexciton rows over 9 slices) are paired, so one L2 read of a slice feeds two rows. Units
-// (pair cost 2, single cost 1) go to the least-loaded wave, longest first. Each wave's list ends with slice -1.
-static std::vector<int4> pt_row_units(const std::vector<int>& gmap, int NW, int pair) {
+// PTs, e.g. 16 biexciton rows over 9 slices) are contracted together in units of up to rmax rows, so one L2
+// read of a slice feeds all of them. Units (cost = rows) go to the least-loaded wave, largest first. A unit is
+// (slice, row 0, row 1 or -1, row 2 | row 3 << 16 or -1, a missing row 3 being 0x7FFF); each wave's list ends
+// with slice -1.
+static std::vector<int4> pt_row_units(const std::vector<int>& gmap, int NW, int rmax) {
     const int N2 = (int)gmap.size();
     std::vector<int4> units;
     std::vector<int> done(N2, 0);
     for (int a = 0; a < N2; ++a) {
         if (done[a]) continue;
-        done[a] = 1;
-        int b = -1;
-        if (pair)
-            for (int c = a + 1; c < N2; ++c)
-                if (!done[c] && gmap[c] == gmap[a]) { b = c; done[c] = 1; break; }
-        units.push_back(make_int4(gmap[a], a, b, 0));
+        int rows[4] = {-1, -1, -1, -1}, cnt = 0;
+        for (int c = a; c < N2 && cnt < rmax; ++c)
+            if (!done[c] && gmap[c] == gmap[a]) { done[c] = 1; rows[cnt++] = c; }
+        const int w = cnt > 2 ? (rows[2] | ((cnt > 3 ? rows[3] : 0x7FFF) << 16)) : -1;
+        units.push_back(make_int4(gmap[a], rows[0], rows[1], w));
     }
-    std::stable_sort(units.begin(), units.end(), [](const int4& x, const int4& y) { return (x.z >= 0) > (y.z >= 0); });
+    auto cost = [](const int4& e) { return e.z < 0 ? 1 : e.w < 0 ? 2 : (e.w >> 16) == 0x7FFF ? 3 : 4; };
+    std::stable_sort(units.begin(), units.end(), [&](const int4& x, const int4& y) { return cost(x) > cost(y); });
     std::vector<std::vector<int4>> per(NW);
     std::vector<int> load(NW, 0);
     for (const int4& e : units) {
@@ -387,11 +389,11 @@ static std::vector<int4> pt_row_units(const std::vector<int>& gmap, int NW, int 
         for (int k = 1; k < NW; ++k)
             if (load[k] < load[w]) w = k;
         per[w].push_back(e);
-        load[w] += e.z >= 0 ? 2 : 1;
+        load[w] += cost(e);
     }
     size_t umax = 1;
     for (auto& v : per) umax = std::max(umax, v.size() + 1);
-    std::vector<int4> out((size_t)NW * umax, make_int4(-1, -1, -1, 0));
+    std::vector<int4> out((size_t)NW * umax, make_int4(-1, 0, -1, -1));
     for (int w = 0; w < NW; ++w)
         for (size_t k = 0; k < per[w].size(); ++k) out[(size_t)w * umax + k] = per[w][k];
     return out;
@@ -571,7 +573,9 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     { const char* c3 = getenv("PQD_CMUL3"); sp.cmul3 = c3 ? atoi(c3) : 1; }
     if (pt && (sp.pt_mode == 4 || sp.pt_mode == 5)) {
         const int nw = P->BT * sweep_wpt(P->BT, P->CHI);
-        std::vector<int4> u = pt_row_units(pt->gmap_h, nw, getenv("PQD_ROWPAIR") ? atoi(getenv("PQD_ROWPAIR")) : 1);
+        int rmax = sweep_rmax(P->N2, P->BT, P->CHI);
+        if (const char* e = getenv("PQD_ROWPAIR")) rmax = std::max(1, std::min(rmax, atoi(e) ? rmax : 1));
+        std::vector<int4> u = pt_row_units(pt->gmap_h, nw, rmax);
         HIPCHK(P->units.upload(u.data(), u.size(), s));
         sp.units = P->units.p;
         sp.umax = (int)(u.size() / nw);

@@ -16,7 +16,7 @@
 //     tile by default), no cross-wave traffic, no barrier inside the phase; steps without MTOs apply the
 //     fused operator F(n) = M_a(n) M_b(n-1) once;
 //   * PT contraction (row alpha of all BT trajectories times the chi x chi slice Q[g(alpha)]): waves take the
-//     rows (or pairs of rows sharing a dictionary slice) of a host-built unit list; v_mfma_f64_4x4x4_4b with
+//     rows (or up to 4 rows sharing a dictionary slice) of a host-built unit list; v_mfma_f64_4x4x4_4b with
 //     3 real products per complex product, every slice element read from L2 once per workgroup and step;
 //   * closure + output traces only on steps inside some trajectory's output window.
 // All PT slices / free propagators are shared by every workgroup at the same absolute step, so the
@@ -218,11 +218,12 @@ __device__ __forceinline__ void pt_row_mfma(const double2* __restrict__ Qg, doub
 // pt_row_mfma with three real products per complex product (3M, see col_apply_mfma3): 3 MFMA chains per
 // (row block, column group) instead of 4; (Qr + Qi) and (Xr + Xi) are one VALU add per loaded element.
 // PF = how many k-steps of the PT slice are in flight ahead of the MFMAs (L2 latency hiding).
-// R = 2 contracts two Liouville rows a0, a1 that share one PT slice (dictionary PTs: rows with the same
-// coupling-eigenvalue pair) in one pass, so each slice element loaded from L2 feeds twice the MFMAs.
+// R > 1 contracts R Liouville rows that share one PT slice (dictionary PTs: rows with the same
+// coupling-eigenvalue pair) in one pass, so each slice element loaded from L2 feeds R times the MFMAs.
+// a0..a3 = the R row indices (unused ones ignored).
 template <int CHI, int BT, int RS, int TS, int PF = 1, int R = 1>
-__device__ __forceinline__ void pt_row_mfma3(const double2* __restrict__ Qg, double2* st, int a0, int a1,
-                                             int lane) {
+__device__ __forceinline__ void pt_row_mfma3(const double2* __restrict__ Qg, double2* st, int a0, int a1, int a2,
+                                             int a3, int lane) {
     constexpr int RB = BT / 4, NG = CHI / 16, KSN = CHI / 4;
     const int x = lane & 3, kk = lane >> 4, c16 = lane & 15;
     double p1[R][RB][NG], p2[R][RB][NG], p3[R][RB][NG];
@@ -234,7 +235,9 @@ __device__ __forceinline__ void pt_row_mfma3(const double2* __restrict__ Qg, dou
             for (int g = 0; g < NG; ++g) { p1[r][rb][g] = 0.0; p2[r][rb][g] = 0.0; p3[r][rb][g] = 0.0; }
     const double2* xr[R];
     xr[0] = st + a0 * RS + kk;
-    if constexpr (R == 2) xr[R - 1] = st + a1 * RS + kk;
+    if constexpr (R >= 2) xr[1] = st + a1 * RS + kk;
+    if constexpr (R >= 3) xr[2] = st + a2 * RS + kk;
+    if constexpr (R >= 4) xr[3] = st + a3 * RS + kk;
     const double2* qp = Qg + (size_t)kk * CHI + c16;
     double2 qn[PF][NG];
 #pragma unroll
@@ -271,13 +274,33 @@ __device__ __forceinline__ void pt_row_mfma3(const double2* __restrict__ Qg, dou
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        double2* wr = st + (r == 0 ? a0 : a1) * RS + c16;
+        double2* wr = st + (r == 0 ? a0 : r == 1 ? a1 : r == 2 ? a2 : a3) * RS + c16;
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
             for (int g = 0; g < NG; ++g)
                 wr[(4 * rb + kk) * TS + 16 * g] = make_double2(p1[r][rb][g] - p2[r][rb][g],
                                                                p3[r][rb][g] - p1[r][rb][g] - p2[r][rb][g]);
+    }
+}
+
+// a unit of n rows sharing one slice (n <= sweep_rmax: the accumulators stay within 48 doubles)
+template <int N2, int CHI, int BT, int RS, int TS, int PF>
+__device__ __forceinline__ void pt_rows3(const double2* __restrict__ Qg, double2* st, int4 e, int lane) {
+    constexpr int RM = sweep_rmax(N2, BT, CHI);
+    if constexpr (RM >= 4) {
+        if (e.w >= 0) {  // rows 2 (and 3) in the low (high) 16 bits of w
+            const int a2 = e.w & 0xFFFF, a3 = e.w >> 16;
+            if (a3 != 0x7FFF) pt_row_mfma3<CHI, BT, RS, TS, PF, 4>(Qg, st, e.y, e.z, a2, a3, lane);
+            else pt_row_mfma3<CHI, BT, RS, TS, PF, 3>(Qg, st, e.y, e.z, a2, a2, lane);
+            return;
+        }
+    }
+    if constexpr (RM >= 2) {
+        if (e.z >= 0) pt_row_mfma3<CHI, BT, RS, TS, PF, 2>(Qg, st, e.y, e.z, e.z, e.z, lane);
+        else pt_row_mfma3<CHI, BT, RS, TS, PF, 1>(Qg, st, e.y, e.y, e.y, e.y, lane);
+    } else {
+        pt_row_mfma3<CHI, BT, RS, TS, PF, 1>(Qg, st, e.y, e.y, e.y, e.y, lane);
     }
 }
 
@@ -422,7 +445,19 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(BT, CHI)) void pt_sweep_kernel(
                     // fused trajectories still hold the state before M_b(n-1): read it through W(n)
                     const double2* ov = (s_fz[b] ? Wg + (size_t)s_sys[b] * p.w_stride + (size_t)n * p.n_out * N2
                                                  : p.ovec) + (size_t)k * N2;
-                    for (int a = 0; a < N2; ++a) c_fma(s, ov[a], rbuf[b * N2 + a]);
+                    // all of a chunk's row loads are issued before its first FMA (one memory round trip per
+                    // chunk, not one per few elements: the scheduler otherwise interleaves them)
+                    constexpr int CK = N2 <= 16 ? N2 : 9;
+#pragma unroll
+                    for (int a0 = 0; a0 < N2; a0 += CK) {
+                        double2 ovr[CK];
+#pragma unroll
+                        for (int j = 0; j < CK; ++j) ovr[j] = (a0 + j < N2) ? ov[a0 + j] : c_zero();
+                        asm volatile("" ::: "memory");
+#pragma unroll
+                        for (int j = 0; j < CK; ++j)
+                            if (a0 + j < N2) c_fma(s, ovr[j], rbuf[b * N2 + a0 + j]);
+                    }
                     outg[s_wo[b] + (long long)(n - s_wb[b]) * p.n_out + k] = s;
                 }
             }
@@ -454,19 +489,14 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(BT, CHI)) void pt_sweep_kernel(
             // the others on the VALU, alternating per row), so the two FP64 pipes of a SIMD run concurrently
             int parity = (p.pt_mode == 2) ? ((wave >= NW / 2) ? 1 : 0) : 0;
             if (p.units && (p.pt_mode == 4 || p.pt_mode == 5)) {
-                // 3M rows by the host's per-wave unit list: (slice, row, second row sharing the slice or -1)
+                // 3M rows by the host's per-wave unit list: (slice, row 0, row 1 or -1, rows 2 | 3 << 16 or -1)
                 const int4* U = p.units + (size_t)wave * p.umax;
                 for (int u = 0; u < p.umax; ++u) {
                     const int4 e = U[u];
                     if (e.x < 0) break;
                     const double2* Qg = Qs + (size_t)e.x * CHI * CHI;
-                    if (p.pt_mode == 5) {
-                        if (e.z >= 0) pt_row_mfma3<CHI, BT, RS, TS, 2, 2>(Qg, st, e.y, e.z, lane);
-                        else pt_row_mfma3<CHI, BT, RS, TS, 2, 1>(Qg, st, e.y, e.y, lane);
-                    } else {
-                        if (e.z >= 0) pt_row_mfma3<CHI, BT, RS, TS, 1, 2>(Qg, st, e.y, e.z, lane);
-                        else pt_row_mfma3<CHI, BT, RS, TS, 1, 1>(Qg, st, e.y, e.y, lane);
-                    }
+                    if (p.pt_mode == 5) pt_rows3<N2, CHI, BT, RS, TS, 2>(Qg, st, e, lane);
+                    else pt_rows3<N2, CHI, BT, RS, TS, 1>(Qg, st, e, lane);
                 }
             } else
             for (int a = wave; a < N2; a += NW) {
@@ -474,11 +504,11 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(BT, CHI)) void pt_sweep_kernel(
                 const bool use_mfma = (p.pt_mode == 1) || (p.pt_mode == 2 && parity == 0);
                 parity ^= 1;
                 if (p.pt_mode == 4) {
-                    pt_row_mfma3<CHI, BT, RS, TS, 1>(Qg, st, a, a, lane);
+                    pt_row_mfma3<CHI, BT, RS, TS, 1>(Qg, st, a, a, a, a, lane);
                     continue;
                 }
                 if (p.pt_mode == 5) {   // 3M with two k-steps of the slice in flight
-                    pt_row_mfma3<CHI, BT, RS, TS, 2>(Qg, st, a, a, lane);
+                    pt_row_mfma3<CHI, BT, RS, TS, 2>(Qg, st, a, a, a, a, lane);
                     continue;
                 }
                 if constexpr (BT == 8) {

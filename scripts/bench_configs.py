@@ -6,6 +6,8 @@ algorithmic flops (fused half steps: F = 8 (D chi^2 + chi N^4 + n_out N^2), D = 
   c2      TLS, N=2, synthetic chi=32 PT, 10,000 steps, 2048 trajectories (area scan)
   c3one   biexciton, N=4, chi=64, 10,000 steps, ONE trajectory (the reference's single-run case: latency)
   c5      six-level linear model, N=6, chi=64, 32 scan points x 64 t1 points = 2048 trajectories, 2,000 tau steps
+  c5d     c5 with a dictionary PT (9 slices for the 36 rows, as a generated physical PT has)
+  c3d     the bench workload at n_tau = 2,000 with a dictionary PT (9 slices for the 16 rows)
 usage: python scripts/bench_configs.py [--configs c1,c2,c3one,c5] [--steps 3]
 """
 import argparse
@@ -29,7 +31,7 @@ def _xy(p, t):
     return p.polar_x * f, p.polar_y * f
 
 
-def workload(model, n_scan, n_t1, n_tau, chi, dt=0.1):
+def workload(model, n_scan, n_t1, n_tau, chi, dt=0.1, dictionary=False):
     from pyaceqd_amd import engine, opgrammar, pt as ptmod
     from pyaceqd_amd.constants import hbar
     from pyaceqd_amd.pulses import ChirpedPulse, PulseTrain
@@ -74,7 +76,8 @@ def workload(model, n_scan, n_t1, n_tau, chi, dt=0.1):
     grid = engine.Grid(0.0, dt, n_steps, 1)
     pt = None
     if chi > 1:
-        pt = ptmod.synthetic_pt(mat(bo), chi=chi, n_init=min(410, n_steps), n_rep=1, seed=1234, eps=0.05, dt=dt)
+        pt = ptmod.synthetic_pt(mat(bo), chi=chi, n_init=min(410, n_steps), n_rep=1, seed=1234, eps=0.05, dt=dt,
+                               dictionary=dictionary)
     mtos, beg, end, sysidx = [], [], [], []
     for k in range(n_scan):
         for t1 in range(n_t1):
@@ -96,6 +99,8 @@ CONFIGS = {
     "c2": dict(model="tls", n_scan=2048, n_t1=1, n_tau=10000, chi=32),
     "c3one": dict(model="biexciton", n_scan=1, n_t1=1, n_tau=10000, chi=64),
     "c5": dict(model="sixls", n_scan=32, n_t1=64, n_tau=2000, chi=64),
+    "c5d": dict(model="sixls", n_scan=32, n_t1=64, n_tau=2000, chi=64, dictionary=True),
+    "c3d": dict(model="biexciton", n_scan=8, n_t1=256, n_tau=2000, chi=64, dictionary=True),
 }
 
 
