@@ -81,6 +81,7 @@ struct SweepParams {
     const int4* units;       // 3M PT rows per wave: [waves][umax] (slice, row 0, row 1 or -1, row 2 | row 3 << 16 or -1;
                              //   a missing row 3 is 0x7FFF),
     int umax;                //   a unit with slice < 0 ends a wave's list; NULL: rows a = wave + k BT
+    int trpre;               // 1: traces one lane per (trajectory, output, row), W rows fetched a step ahead
     int ablate;              // diagnostics only (PQD_ABLATE): 1 skip PT, 2 skip column phases, 4 skip outputs
 };
 

@@ -571,6 +571,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     { const char* ab = getenv("PQD_ABLATE"); sp.ablate = ab ? atoi(ab) : 0; }
     { const char* pm = getenv("PQD_PT_MODE"); sp.pt_mode = pm ? atoi(pm) : 4; }
     { const char* c3 = getenv("PQD_CMUL3"); sp.cmul3 = c3 ? atoi(c3) : 1; }
+    { const char* tp = getenv("PQD_TRPRE"); sp.trpre = tp ? atoi(tp) : 1; }
     if (pt && (sp.pt_mode == 4 || sp.pt_mode == 5)) {
         const int nw = P->BT * sweep_wpt(P->BT, P->CHI);
         int rmax = sweep_rmax(P->N2, P->BT, P->CHI);
@@ -581,6 +582,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
         sp.umax = (int)(u.size() / nw);
     }
     { const char* fz = getenv("PQD_FUSE"); sp.fuse = (!P->nopt && ns > 0 && (fz ? atoi(fz) : 1)) ? 1 : 0; }
+    if (!sp.fuse) sp.trpre = 0;  // the prefetched rows are W(n), which exists only with fused half steps
     if (sp.fuse) {
         HIPCHK(P->F.alloc((size_t)n_sys * ns * m2));
         HIPCHK(P->W.alloc((size_t)n_sys * (ns + 1) * n_out * N2));

@@ -414,6 +414,11 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(BT, CHI)) void pt_sweep_kernel(
     __syncthreads();
 
     const int pj = lane & 15, pq = lane >> 4;
+    // traces with one lane per (trajectory, output, row) when N2 is a power of two and they fit the workgroup
+    // (16-lane reduction groups); each lane keeps the next step's W row element in a register
+    const int ntr = BT * p.n_out * N2;
+    const bool lanetr = (N2 == 4 || N2 == 16) && p.trpre && ntr <= NT;
+    double2 wpre = c_zero();
     bool fz = false;  // this wave's trajectory sits between M_b(n-1) and M_a(n) unapplied (fused step n)
     for (int n = 0;; ++n) {
         // ------------------------------------------------------------ outputs at step n
@@ -438,6 +443,17 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(BT, CHI)) void pt_sweep_kernel(
                 if (e < NPART && qr == 0) rbuf[row] = s;
             }
             __syncthreads();
+            if (lanetr) {
+                // one lane per (trajectory, output, row): the row element of W(n) was fetched a step ahead
+                if (tid < ntr) {
+                    const int a = tid % N2, bk = tid / N2, b = bk / p.n_out, k = bk - (bk / p.n_out) * p.n_out;
+                    const double2 v = s_fz[b] ? wpre : p.ovec[k * N2 + a];
+                    double2 x = c_mul(v, rbuf[b * N2 + a]);
+#pragma unroll
+                    for (int m = 1; m < N2; m <<= 1) x = c_add(x, c_shfl_xor(x, m));
+                    if (a == 0 && s_wb[b] <= n && n <= s_we[b]) outg[s_wo[b] + (long long)(n - s_wb[b]) * p.n_out + k] = x;
+                }
+            } else
             for (int e = tid; e < BT * p.n_out; e += NT) {
                 const int b = e / p.n_out, k = e - (e / p.n_out) * p.n_out;
                 if (s_wb[b] <= n && n <= s_we[b]) {
@@ -463,6 +479,10 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(BT, CHI)) void pt_sweep_kernel(
             }
         }
         if (n >= n_end) break;
+        if (lanetr && tid < ntr) {  // W(n + 1) row element for the next step's traces (fused trajectories)
+            const int a = tid % N2, bk = tid / N2, b = bk / p.n_out, k = bk - (bk / p.n_out) * p.n_out;
+            wpre = Wg[(size_t)s_sys[b] * p.w_stride + ((size_t)(n + 1) * p.n_out + k) * N2 + a];
+        }
 
         // ------------------------------------------------------------ column phase A
         const double2* Ma = Mg + (size_t)(2 * n) * N2 * N2;

@@ -325,7 +325,7 @@ def test_sweep_pt_bt8(monkeypatch, N, chi):
 @pytest.mark.parametrize("with_pt", [False, True])
 def test_multi_system_scan(monkeypatch, with_pt, bt, fuse):
     """trajectories of several systems; workgroups straddle systems (each wave reads its own system's free
-    propagators and fused output maps)"""
+    propagators and fused output maps; the lane-parallel traces prefetch each trajectory's own W rows)"""
     monkeypatch.setenv("PQD_BT", bt)
     monkeypatch.setenv("PQD_FUSE", fuse)
     N = 4
@@ -340,11 +340,13 @@ def test_multi_system_scan(monkeypatch, with_pt, bt, fuse):
               oracle.propagate(systems, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
 
 
+@pytest.mark.parametrize("trpre", ["0", "1"])
 @pytest.mark.parametrize("fuse", ["0", "1"])
-def test_bench_workload_small_vs_oracle(monkeypatch, fuse):
+def test_bench_workload_small_vs_oracle(monkeypatch, fuse, trpre):
     """the bench workload itself (scan of G2 sweeps, chi=64, B=8 path) at reduced n_tau vs the oracle,
     with the fused half steps (default) and without"""
     monkeypatch.setenv("PQD_FUSE", fuse)
+    monkeypatch.setenv("PQD_TRPRE", trpre)
     import bench
     systems, grid, pt, rho0, ops, tr = bench.build_workload(16, 60, 64, scan=2)
     plan = engine.Plan(systems, grid, rho0, ops, tr, pt=pt)
