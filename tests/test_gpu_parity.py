@@ -381,6 +381,24 @@ def test_sweep_pt_contraction_modes(monkeypatch, pt_mode, bt, N, chi, fuse):
               oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
 
 
+@pytest.mark.parametrize("cfg", ["c1", "c2", "c3one", "c5", "c5d", "c3d"])
+def test_config_workloads_small_vs_oracle(cfg):
+    """the SURVEY §8d configurations measured by scripts/bench_configs.py, at reduced scan size
+    and step count, vs the oracle: one system per trajectory (c1, c2), a single trajectory (c3one), the six-level
+    G2 scan at N^2 = 36 with and without a dictionary PT (c5, c5d: units of up to 4 rows per slice), the
+    biexciton scan with a dictionary PT (c3d)"""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+    import bench_configs
+    c = dict(bench_configs.CONFIGS[cfg])
+    c["n_scan"] = min(c["n_scan"], 5)
+    c["n_t1"] = min(c["n_t1"], 7)
+    c["n_tau"] = 40
+    N, sysd, grid, pt, rho0, ops, tr = bench_configs.workload(**c)
+    cmp_lists(engine.propagate(sysd, grid, rho0, ops, tr, pt=pt),
+              oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
+
+
 # --------------------------------------------------------------------------------- generated phonon PTs
 def test_tls_phonons_generated_pt_vs_oracle(monkeypatch, tmp_path):
     """config C2 shape: tls with a generated QD-phonon PT (pyaceqd_amd.ptgen, bond capped at 32 by the threshold
