@@ -174,6 +174,13 @@ int pqd_dynamics_t1(pqd_ctx* ctx, const pqd_c128* dm_1, const pqd_c128* dm_2, co
                     const double* t1, const pqd_c128* precalc, int32_t n_t, double dt, int32_t n_map,
                     int32_t dim, double tb, int32_t n_precalc, pqd_c128* result);
 
+/* ---- time-local dynamical maps (replaces tools.calc_tl_dynmap_pseudo, reference tools.py:446-484) ----
+ * dm: n_maps row-major n x n maps, dm[i] = E(t_{i+1}, t0). out (n_maps maps): out[0] = dm[0],
+ * out[i] = dm[i] pinv(dm[i-1]) with singular values <= rcond * max(s) dropped (numpy pinv, rcond
+ * 1e-12 in the reference). n <= 36 (N <= 6). */
+int pqd_tl_dynmap_pseudo(pqd_ctx* ctx, const pqd_c128* dm, int32_t n_maps, int32_t n, double rcond,
+                         pqd_c128* out);
+
 #ifdef __cplusplus
 }
 #endif

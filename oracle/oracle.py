@@ -260,3 +260,14 @@ def dynamics_t1(dm_1, dm_2, rho_init, t1, precalc, dt, dim, tb):
                          C.c_double(dt), C.c_int(dm_1.shape[2]), C.c_int(dim), C.c_double(tb),
                          C.c_int(precalc.shape[2]), _fp(out))
     return out
+
+
+def tl_dynmap_pseudo(dm, n_out=None, rcond=1e-12):
+    """time-local maps out[i] = dm[i] pinv(dm[i-1], rcond), out[0] = dm[0] — numpy restatement of
+    calc_tl_dynmap_pseudo (reference pyaceqd/tools.py:446-484, LAPACK SVD inside numpy's pinv)"""
+    n_out = len(dm) if n_out is None else n_out
+    out = np.empty((n_out,) + dm.shape[1:], dtype=np.complex128)
+    out[0] = dm[0]
+    for i in range(1, n_out):
+        out[i] = dm[i] @ np.linalg.pinv(dm[i - 1], rcond=rcond)
+    return out

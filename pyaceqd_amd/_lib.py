@@ -90,6 +90,7 @@ _SIGS = {
                        C.c_int32, P_C128, C.c_double, C.c_int32, P_C128], C.c_int),
     "pqd_dynamics_t1": ([C.c_void_p, P_C128, P_C128, P_C128, P_F64, P_C128, C.c_int32, C.c_double, C.c_int32,
                          C.c_int32, C.c_double, C.c_int32, P_C128], C.c_int),
+    "pqd_tl_dynmap_pseudo": ([C.c_void_p, P_C128, C.c_int32, C.c_int32, C.c_double, P_C128], C.c_int),
 }
 
 EXPORTED = tuple(_SIGS)

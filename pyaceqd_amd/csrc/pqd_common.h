@@ -146,4 +146,6 @@ hipError_t launch_four_time(const FourTimeParams& p, hipStream_t s);
 hipError_t launch_propagate_tau(int N2, const double2* dm, const double2* rho0, int n_tau, int j_start,
                                 double2* out, hipStream_t s);
 hipError_t launch_dynamics_t1(const FourTimeParams& p, double2* out, hipStream_t s);
+hipError_t launch_tl_dynmap(const double2* dm, int n_maps, int n, double rcond, double2* out, hipStream_t s);
+int tl_dynmap_nmax();
 bool sweep_supported(int N2, int CHI);

@@ -863,4 +863,24 @@ int pqd_dynamics_t1(pqd_ctx* ctx, const pqd_c128* dm_1, const pqd_c128* dm_2, co
     return four_time_common(ctx, p, dm_1, dm_2, rho_init, t1, precalc, nullptr, 0, result, true);
 }
 
+int pqd_tl_dynmap_pseudo(pqd_ctx* ctx, const pqd_c128* dm, int32_t n_maps, int32_t n, double rcond,
+                         pqd_c128* out) {
+    if (!ctx || !dm || !out) return fail(PQD_ERR_ARG, "NULL argument");
+    if (n < 1 || n > tl_dynmap_nmax()) return fail(PQD_ERR_UNSUPPORTED, "map size %d (max %d)", n, tl_dynmap_nmax());
+    if (n_maps < 0) return fail(PQD_ERR_ARG, "n_maps %d", n_maps);
+    if (!(rcond >= 0.0)) return fail(PQD_ERR_ARG, "rcond %g", rcond);
+    if (n_maps == 0) return PQD_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const size_t m2 = (size_t)n * n;
+    DevBuf<double2> d, o;
+    HIPCHK(d.upload(reinterpret_cast<const double2*>(dm), (size_t)n_maps * m2, s));
+    HIPCHK(o.alloc((size_t)n_maps * m2));
+    HIPCHK(hipMemcpyAsync(o.p, d.p, m2 * sizeof(double2), hipMemcpyDeviceToDevice, s));  // out[0] = dm[0]
+    HIPCHK(launch_tl_dynmap(d.p, n_maps, n, rcond, o.p, s));
+    HIPCHK(hipMemcpyAsync(out, o.p, (size_t)n_maps * m2 * sizeof(double2), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return PQD_OK;
+}
+
 }  // extern "C"

@@ -172,17 +172,25 @@ def op_to_matrix(op):
 
 # ------------------------------------------------------------------------- dynamical maps
 def calc_tl_dynmap_pseudo(dm, times, debug=False):
-    """Time-local maps E(t_{i+1}, t_i) = E(t_{i+1}, t0) pinv(E(t_i, t0)) from cumulative maps dm[i] = E(t_{i+1}, t0)."""
-    n = dm.shape[1]
-    out = np.zeros((len(times) - 1, n, n), dtype=complex)
-    out[0] = dm[0]
-    for i in range(1, len(out)):
-        try:
-            out[i] = dm[i] @ np.linalg.pinv(dm[i - 1], rcond=1e-12)
-        except np.linalg.LinAlgError:
-            out[i] = dm[i] @ np.linalg.pinv(dm[i - 1])
-            if debug:
-                print("Singular matrix at time = {}, index: {}".format(times[i], i))
+    """Time-local maps E(t_{i+1}, t_i) = E(t_{i+1}, t0) pinv(E(t_i, t0)) from cumulative maps dm[i] = E(t_{i+1}, t0)
+    (reference tools.py:446-484): out[0] = dm[0], out[i] = dm[i] pinv(dm[i-1], rcond=1e-12), len(times)-1 maps.
+
+    Runs on the GPU (libpqd `pqd_tl_dynmap_pseudo`: one Jacobi SVD per map, one workgroup each). The reference's
+    LinAlgError retry without rcond has no counterpart: the Jacobi SVD does not fail to converge; `debug` is
+    accepted for signature compatibility."""
+    from . import _lib
+    dm = np.ascontiguousarray(dm, dtype=np.complex128)
+    n_out = len(times) - 1
+    if dm.ndim != 3 or dm.shape[1] != dm.shape[2]:
+        raise ValueError(f"dm must be (n_t, n, n), got {dm.shape}")
+    if n_out < 1 or dm.shape[0] < n_out:
+        raise ValueError(f"need len(times)-1 = {n_out} >= 1 maps, dm has {dm.shape[0]}")
+    dm = np.ascontiguousarray(dm[:n_out])
+    out = np.empty_like(dm)
+    ctx = _lib.context()
+    with ctx.lock:
+        _lib.check(_lib.lib().pqd_tl_dynmap_pseudo(ctx.handle, _lib.cptr(dm), int(n_out), int(dm.shape[1]),
+                                                   1e-12, _lib.cptr(out)))
     return out
 
 

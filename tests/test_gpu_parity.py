@@ -225,6 +225,48 @@ def test_mapchain_large_vs_oracle():
     assert rel(a, b) < 1e-11
 
 
+# --------------------------------------------------------------------------------- time-local maps
+def test_tl_dynmap_vs_reference_golden(golden_dir):
+    """GPU Jacobi-SVD pinv time-localisation vs the reference's calc_tl_dynmap_pseudo (tools.py:446-484)
+    at map sizes 4/16/25/36, including rank-deficient maps where the rcond=1e-12 cut-off drops 3 singular
+    values (tests/golden/make_golden_tlmap.py, pyref_tools.npz)"""
+    from pyaceqd_amd import tools as T
+    z = load(golden_dir, "pyref_tlmap.npz")
+    for name in ("d4", "d5", "d6", "rank2", "rank4"):
+        got = T.calc_tl_dynmap_pseudo(z[f"{name}_dm"], z[f"{name}_times"])
+        assert got.shape == z[f"{name}_tl"].shape
+        assert rel(got, z[f"{name}_tl"]) < 1e-10, name
+    z = load(golden_dir, "pyref_tools.npz")
+    assert rel(T.calc_tl_dynmap_pseudo(z["dm_cum"], z["tl_times"]), z["tl_maps"]) < 1e-10
+    # fewer maps than times-1 is an error, as the reference's indexing would be
+    with pytest.raises(ValueError):
+        T.calc_tl_dynmap_pseudo(z["dm_cum"][:3], z["tl_times"])
+
+
+@pytest.mark.parametrize("dim,n_maps", [(2, 3000), (4, 3000), (6, 400)])
+def test_tl_dynmap_large_vs_oracle(dim, n_maps):
+    """long map chains: GPU vs the numpy-pinv oracle, and the size-independent property that
+    time-localising the cumulative products of per-step maps gives back those maps"""
+    from pyaceqd_amd import tools as T
+    rng = np.random.default_rng(dim)
+    N2 = dim * dim
+    G = 0.05 * (rng.normal(size=(N2, N2)) + 1j * rng.normal(size=(N2, N2)))
+    steps = np.empty((n_maps, N2, N2), dtype=complex)
+    import scipy.linalg as sla
+    base = sla.expm(G - G.conj().T)  # unitary: the cumulative maps stay well conditioned
+    for i in range(n_maps):
+        steps[i] = base @ (np.eye(N2) + 1e-3 * np.sin(0.01 * i) * (G + G.conj().T))
+    dm = np.empty_like(steps)
+    acc = np.eye(N2, dtype=complex)
+    for i in range(n_maps):
+        acc = steps[i] @ acc
+        dm[i] = acc
+    times = np.round(np.arange(n_maps + 1) * 0.1, 6)
+    got = T.calc_tl_dynmap_pseudo(dm, times)
+    assert rel(got, oracle.tl_dynmap_pseudo(dm)) < 1e-9
+    assert rel(got, steps) < 1e-9
+
+
 # --------------------------------------------------------------------------------- drop-in driver
 def _oracle_patch(monkeypatch):
     """route general_system's propagate through the oracle (same lowering, CPU arithmetic)"""
