@@ -148,4 +148,7 @@ hipError_t launch_propagate_tau(int N2, const double2* dm, const double2* rho0, 
 hipError_t launch_dynamics_t1(const FourTimeParams& p, double2* out, hipStream_t s);
 hipError_t launch_tl_dynmap(const double2* dm, int n_maps, int n, double rcond, double2* out, hipStream_t s);
 int tl_dynmap_nmax();
+bool split_supported(int N2, int CHI, int n_traj, int n_cu);
+hipError_t launch_split(int N2, int CHI, int n_traj, const SweepParams& p, double2* X, unsigned* cnt,
+                        unsigned* err, hipStream_t s);
 bool sweep_supported(int N2, int CHI);

@@ -204,6 +204,9 @@ struct pqd_plan {
     pqd_ctx* ctx = nullptr;
     int N2 = 0, CHI = 1, BT = 4, n_traj = 0, n_blocks = 0, n_steps = 0, n_sys = 1;
     bool nopt = true;
+    bool split = false;  // small batch: one trajectory over N2 workgroups (pt_split.hip)
+    DevBuf<double2> Xs;
+    DevBuf<unsigned> cnt, err;
     DevBuf<double2> L0, S, T, samples, M, F, W, rho0, ovec, sop, out;
     DevBuf<FreePropSys> systab;
     FuseParams fu{};
@@ -527,6 +530,15 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess) n_cu = prop.multiProcessorCount;
     }
+    // latency path: a batch of at most split_max trajectories spreads each over N2 workgroups
+    // (PQD_SPLIT: 0 off, 1 auto, 2 whenever the device holds the groups)
+    {
+        const char* e = getenv("PQD_SPLIT");
+        const int mode = e ? atoi(e) : 1;
+        const int split_max = 8;
+        P->split = pt && mode != 0 && split_supported(N2, P->CHI, tr->n_traj, n_cu) &&
+                   (mode == 2 || tr->n_traj <= split_max);
+    }
     int BT = (sweep_max_bt(N2) >= 8 && tr->n_traj >= 8 * n_cu) ? 8 : 4;
     if (const char* e = getenv("PQD_BT")) BT = std::min(atoi(e) >= 8 ? 8 : 4, sweep_max_bt(N2));
     if (P->CHI > 64) BT = 4;  // chi = 128: only four augmented states fit the LDS
@@ -592,6 +604,11 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     }
     sp.F = P->F.p; sp.W = P->W.p;
     sp.woff = P->woff.p; sp.ev_start = P->ev_start.p; sp.ev = P->ev.p; sp.sop = P->sop.p; sp.out = P->out.p;
+    if (P->split) {
+        HIPCHK(P->Xs.alloc((size_t)P->n_traj * 2 * N2 * P->CHI));
+        HIPCHK(P->cnt.alloc((size_t)P->n_traj * 32));
+        HIPCHK(P->err.alloc(4));
+    }
     HIPCHK(hipStreamSynchronize(s));
     *out = guard.release();
     return PQD_OK;
@@ -617,6 +634,8 @@ int pqd_plan_execute(pqd_plan* P, int32_t rebuild_free) {
     HIPCHK(hipEventRecord(e[1], s));
     if (P->nopt)
         HIPCHK(launch_sweep_nopt(P->N2, P->n_traj, P->sp, s));
+    else if (P->split)
+        HIPCHK(launch_split(P->N2, P->CHI, P->n_traj, P->sp, P->Xs.p, P->cnt.p, P->err.p, s));
     else
         HIPCHK(launch_sweep(P->N2, P->CHI, P->BT, P->n_blocks, P->sp, s));
     HIPCHK(hipEventRecord(e[2], s));
@@ -633,7 +652,10 @@ int pqd_plan_download(pqd_plan* P, pqd_c128* out, int64_t out_len) {
     HIPCHK(hipSetDevice(P->ctx->device));
     if (P->out_len > 0)
         HIPCHK(hipMemcpyAsync(out, P->out.p, P->out_len * sizeof(double2), hipMemcpyDeviceToHost, P->ctx->stream));
+    unsigned err = 0;
+    if (P->split) HIPCHK(hipMemcpyAsync(&err, P->err.p, sizeof(unsigned), hipMemcpyDeviceToHost, P->ctx->stream));
     HIPCHK(hipStreamSynchronize(P->ctx->stream));
+    if (err) return fail(PQD_ERR_HIP, "split sweep: a workgroup group timed out waiting for its peers");
     return PQD_OK;
 }
 

@@ -1,0 +1,290 @@
+// pt_split.hip — latency path for small batches: ONE trajectory spread over G = N2 workgroups.
+//
+// The batched sweep (pt_sweep.hip) gives a trajectory one wave of one workgroup, so a single run
+// (SURVEY §8d C3 "biexciton, chi 64, 1 MI355X": one trajectory) streams the whole PT slice set
+// (N2 chi^2 c128 = 1 MiB per step at N = 4, chi = 64) through ONE CU: ≈13 µs per step.
+// Here workgroup g of a trajectory's group owns PT row alpha = g: it contracts that row with its
+// slice (64 KiB per step at chi = 64, prefetched into registers while the group exchanges). The
+// column phases (M_b(n-1), MTOs, outputs, M_a(n), or the fused F(n) = M_a(n) M_b(n-1)) mix rows, so
+// every workgroup gathers the whole state (N2 x chi, 16 KiB at C3) once per step and runs them
+// redundantly — ONE exchange per step instead of a row/column transpose pair.
+// Hand-off (MI355X_MICROARCH.md § visibility, "Valid forms", table row 1): every payload store is
+// an 8-B relaxed agent-scope atomic (global_store sc1), every storing wave drains with
+// s_waitcnt vmcnt(0), a workgroup barrier, then ONE lane adds to the group's monotonic counter
+// (agent-scope atomic); wave 0 polls it with relaxed agent-scope loads (global_load sc1), the other
+// waves wait at a barrier, and every load of the payload is such an sc1 load — so no fences. The
+// exchange buffer is double-buffered by step parity (a workgroup cannot publish step n+2 before
+// every peer has gathered step n). One workgroup per CU (the LDS request forces it) and at most
+// n_cu workgroups (host check), so every workgroup is resident; every spin is bounded and a
+// timeout ends the kernel with an error word the host turns into PQD_ERR_HIP.
+// Semantics are the sweep's: step n applies M_b(n-1), applyBefore MTOs at n,
+// output(n), applyAfter MTOs at n, M_a(n), PT(n); steps without MTOs use F(n) and read the outputs
+// through W(n) = ovec M_b(n-1), as the batched kernel does.
+#include "pqd_common.h"
+
+namespace {
+
+typedef unsigned long long __attribute__((address_space(1))) gu64;
+typedef unsigned int __attribute__((address_space(1))) gu32;
+
+constexpr int SP_NT = 256;
+constexpr int SP_LDS_FORCE = 96 * 1024;  // dynamic LDS request: one workgroup per CU
+constexpr unsigned SP_SPIN_LIMIT = 1u << 22;
+
+__device__ __forceinline__ void st_sc1(double2* p, double2 v) {
+    __hip_atomic_store((gu64*)&p->x, (unsigned long long)__double_as_longlong(v.x), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu64*)&p->y, (unsigned long long)__double_as_longlong(v.y), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// plain global load (a generic pointer would become flat_load, which also counts in lgkmcnt: every LDS wait
+// would then wait for the register prefetches too)
+__device__ __forceinline__ double2 gld(const double2* p) {
+    const __attribute__((address_space(1))) double* q = (const __attribute__((address_space(1))) double*)p;
+    return make_double2(q[0], q[1]);
+}
+
+__device__ __forceinline__ double2 ld_sc1(const double2* p) {
+    const unsigned long long x = __hip_atomic_load((gu64*)&p->x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long y = __hip_atomic_load((gu64*)&p->y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_double2(__longlong_as_double((long long)x), __longlong_as_double((long long)y));
+}
+
+template <int N2, int CHI>
+struct SplitLayout {
+    static constexpr int KG = SP_NT / CHI;            // k groups of the row contraction
+    static constexpr int KPER = CHI / KG;             // slice rows per thread
+    static constexpr int RPT = (N2 + KG - 1) / KG;    // state rows per thread in the column phase
+    static constexpr int OPER = (N2 * N2 + SP_NT - 1) / SP_NT;  // operator elements per thread
+    static constexpr int LDS_STATE = 2 * N2 * CHI + N2 * N2 + N2 + SP_NT;  // complex elements
+    static constexpr int LDS = (LDS_STATE * 16 > SP_LDS_FORCE) ? LDS_STATE * 16 : SP_LDS_FORCE;
+};
+
+template <int N2, int CHI>
+__global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2* __restrict__ X,
+                                                         unsigned* __restrict__ cnt, unsigned* __restrict__ err) {
+    using L = SplitLayout<N2, CHI>;
+    constexpr int KG = L::KG, KPER = L::KPER, RPT = L::RPT, OPER = L::OPER;
+    constexpr int G = N2, E = N2 * CHI;
+    extern __shared__ __attribute__((aligned(16))) double2 smem[];
+    // smem: full state ping-pong [0, E) and [E, 2E), staged column operator, closure contractions r[beta]
+    // (output phase), PT partial sums — all indexed off smem so every access stays ds_*
+    constexpr int OPO = 2 * E, RRO = OPO + N2 * N2, REDO = RRO + N2;
+    __shared__ int s_abort;
+
+    const int tid = threadIdx.x;
+    const int t = blockIdx.x / G, g = blockIdx.x - t * G;
+    const int wb = p.wbeg[t], we = p.wend[t];
+    const long long wo = p.woff[t];
+    const int sy = p.traj_sys[t];
+    const double2* __restrict__ Mg = p.M + (size_t)sy * p.m_stride;
+    const double2* __restrict__ Fg = p.F + (size_t)sy * p.f_stride;
+    const double2* __restrict__ Wg = p.W + (size_t)sy * p.w_stride;
+    double2* __restrict__ Xt = X + (size_t)t * 2 * E;
+    unsigned* ct = cnt + (size_t)t * 32;  // one 128-B line per group counter
+    const int n_end = we;
+    constexpr int m2 = N2 * N2;
+    const int ev_lim = p.ev_start[t + 1];
+    int ev_cur = p.ev_start[t];
+    const int dcol = tid % CHI, kq = tid / CHI;
+
+    int qo = 0, to = E;  // current state / scratch offsets
+    for (int e = tid; e < E; e += SP_NT) {
+        const int a = e / CHI, d = e - (e / CHI) * CHI;
+        smem[qo + e] = c_mul(gld(p.rho0 + a), gld(p.bond0 + d));
+    }
+    // y[a][d] = sum_b Op[a][b] Q[b][d]: thread owns column d and rows kq + KG i
+    auto apply_lds = [&]() {
+        __syncthreads();  // Op staged, Q complete
+        double2 x[N2];
+#pragma unroll
+        for (int b = 0; b < N2; ++b) x[b] = smem[qo + b * CHI + dcol];
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+            const int a = kq + KG * i;
+            if (a < N2) {
+                double2 acc = c_zero();
+#pragma unroll
+                for (int b = 0; b < N2; ++b) c_fma(acc, smem[OPO + a * N2 + b], x[b]);
+                smem[to + a * CHI + dcol] = acc;
+            }
+        }
+        __syncthreads();
+        const int sw = qo; qo = to; to = sw;
+    };
+    auto apply_global = [&](const double2* __restrict__ M) {
+        __syncthreads();  // previous readers of Op done
+#pragma unroll
+        for (int i = 0; i < OPER; ++i) {
+            const int e = tid + SP_NT * i;
+            if (e < m2) smem[OPO + e] = gld(M + e);
+        }
+        apply_lds();
+    };
+    // output(n) through rows w[k][.] (ovec, or W(n) on the state before M_b(n-1)): workgroup 0 writes it
+    auto output = [&](int n, const double2* __restrict__ w) {
+        if (g != 0 || n < wb || n > we) return;
+        const double2* cv = (n == 0) ? p.closure0 : p.closure + (size_t)p.sched[n - 1] * CHI;
+        __syncthreads();
+        if (tid < 4 * N2) {
+            const int b = tid >> 2, q = tid & 3;
+            double2 s = c_zero();
+            for (int d = q; d < CHI; d += 4) c_fma(s, smem[qo + b * CHI + d], gld(cv + d));
+            s = c_add(s, c_shfl_xor(s, 1));
+            s = c_add(s, c_shfl_xor(s, 2));
+            if (q == 0) smem[RRO + b] = s;
+        }
+        __syncthreads();
+        for (int k = tid; k < p.n_out; k += SP_NT) {
+            double2 s = c_zero();
+#pragma unroll
+            for (int b = 0; b < N2; ++b) c_fma(s, gld(w + (size_t)k * N2 + b), smem[RRO + b]);
+            p.out[wo + (long long)(n - wb) * p.n_out + k] = s;
+        }
+    };
+    auto has_event = [&](int n) { return ev_cur < ev_lim && p.ev[ev_cur].x == n; };
+
+    // slice row of PT(0) and the fused operator of step 1
+    double2 sreg[KPER], opreg[OPER];
+    auto fetch_slice = [&](int n) {
+        const double2* __restrict__ S = p.Q + ((size_t)p.sched[n] * p.D + p.gmap[g]) * CHI * CHI;
+#pragma unroll
+        for (int j = 0; j < KPER; ++j) sreg[j] = gld(S + (size_t)(kq * KPER + j) * CHI + dcol);
+    };
+    auto fetch_fused = [&](int n) {
+        const double2* __restrict__ M = Fg + (size_t)n * m2;
+#pragma unroll
+        for (int i = 0; i < OPER; ++i) {
+            const int e = tid + SP_NT * i;
+            opreg[i] = (e < m2) ? gld(M + e) : c_zero();
+        }
+    };
+    if (n_end > 0) fetch_slice(0);
+    bool pre = false;  // opreg holds F(n) of the coming step
+    for (int n = 0;; ++n) {
+        // ---- column phase
+        const bool fz = p.fuse && n >= 1 && !has_event(n);
+        if (fz) {
+            output(n, Wg + (size_t)n * p.n_out * N2);
+            if (n >= n_end) break;
+            __syncthreads();
+            if (pre) {
+#pragma unroll
+                for (int i = 0; i < OPER; ++i) {
+                    const int e = tid + SP_NT * i;
+                    if (e < m2) smem[OPO + e] = opreg[i];
+                }
+                apply_lds();
+            } else {
+                apply_global(Fg + (size_t)n * m2);
+            }
+        } else {
+            if (n > 0) apply_global(Mg + (size_t)(2 * (n - 1) + 1) * m2);
+            while (ev_cur < ev_lim) {  // applyBefore MTOs at n
+                const int4 ev = p.ev[ev_cur];
+                if (ev.x != n || ev.y != 0) break;
+                apply_global(p.sop + (size_t)ev.z * m2);
+                ++ev_cur;
+            }
+            output(n, p.ovec);
+            if (n >= n_end) break;
+            while (ev_cur < ev_lim) {  // applyAfter MTOs at n
+                const int4 ev = p.ev[ev_cur];
+                if (ev.x != n || ev.y != 1) break;
+                apply_global(p.sop + (size_t)ev.z * m2);
+                ++ev_cur;
+            }
+            apply_global(Mg + (size_t)(2 * n) * m2);
+        }
+        // ---- PT row g: y = Q[g][:] . S(n) -> exchange buffer (parity n & 1)
+        double2 acc = c_zero();
+#pragma unroll
+        for (int j = 0; j < KPER; ++j) c_fma(acc, smem[qo + g * CHI + kq * KPER + j], sreg[j]);
+        smem[REDO + tid] = acc;
+        __syncthreads();
+        double2* Xn = Xt + (size_t)(n & 1) * E;
+        if (tid < CHI) {
+            double2 y = smem[REDO + tid];
+#pragma unroll
+            for (int q = 1; q < KG; ++q) y = c_add(y, smem[REDO + q * CHI + tid]);
+            st_sc1(Xn + (size_t)g * CHI + tid, y);
+        }
+        // ---- arrive, prefetch the next step's slice row and fused operator, then wait for the group
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add((gu32*)ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n + 1 < n_end) fetch_slice(n + 1);
+        pre = p.fuse && n + 1 < n_end && !has_event(n + 1);
+        if (pre) fetch_fused(n + 1);
+        if (tid < 64) {
+            const unsigned target = (unsigned)G * (unsigned)(n + 1);
+            unsigned spins = 0;
+            bool ok = true;
+            while (__hip_atomic_load((gu32*)ct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > SP_SPIN_LIMIT) { ok = false; break; }
+            }
+            if (tid == 0) {
+                s_abort = ok ? 0 : 1;
+                if (!ok) __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __syncthreads();
+        if (s_abort) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: payload loads are sc1
+        for (int e = tid; e < E; e += SP_NT) smem[qo + e] = ld_sc1(Xn + e);
+        __syncthreads();
+    }
+}
+
+template <int N2, int CHI>
+hipError_t launch_split_t(int n_traj, const SweepParams& p, double2* X, unsigned* cnt, unsigned* err, hipStream_t s) {
+    using L = SplitLayout<N2, CHI>;
+    static_assert(L::LDS <= 160 * 1024, "LDS budget");
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)pt_split_kernel<N2, CHI>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::LDS);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL((pt_split_kernel<N2, CHI>), dim3(n_traj * N2), dim3(SP_NT), L::LDS, s, p, X, cnt, err);
+    return hipGetLastError();
+}
+
+template <int N2>
+hipError_t launch_split_n(int CHI, int n_traj, const SweepParams& p, double2* X, unsigned* cnt, unsigned* err,
+                          hipStream_t s) {
+    switch (CHI) {
+        case 16: return launch_split_t<N2, 16>(n_traj, p, X, cnt, err, s);
+        case 32: return launch_split_t<N2, 32>(n_traj, p, X, cnt, err, s);
+        case 64: return launch_split_t<N2, 64>(n_traj, p, X, cnt, err, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace
+
+bool split_supported(int N2, int CHI, int n_traj, int n_cu) {
+    return (CHI == 16 || CHI == 32 || CHI == 64) &&
+           (N2 == 4 || N2 == 9 || N2 == 16 || N2 == 25 || N2 == 36) && n_traj >= 1 &&
+           (long long)n_traj * N2 <= n_cu;
+}
+
+// X: n_traj * 2 * N2 * CHI exchange buffer; cnt: n_traj * 32 counters and err, zeroed here before every launch
+hipError_t launch_split(int N2, int CHI, int n_traj, const SweepParams& p, double2* X, unsigned* cnt,
+                        unsigned* err, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(cnt, 0, (size_t)n_traj * 32 * sizeof(unsigned), s);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(err, 0, 4 * sizeof(unsigned), s);
+    if (e != hipSuccess) return e;
+    switch (N2) {
+        case 4: return launch_split_n<4>(CHI, n_traj, p, X, cnt, err, s);
+        case 9: return launch_split_n<9>(CHI, n_traj, p, X, cnt, err, s);
+        case 16: return launch_split_n<16>(CHI, n_traj, p, X, cnt, err, s);
+        case 25: return launch_split_n<25>(CHI, n_traj, p, X, cnt, err, s);
+        case 36: return launch_split_n<36>(CHI, n_traj, p, X, cnt, err, s);
+        default: return hipErrorInvalidValue;
+    }
+}

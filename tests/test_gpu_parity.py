@@ -78,6 +78,40 @@ def test_sweep_pt(N, chi):
               oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt), 1e-11)
 
 
+@pytest.mark.parametrize("N", [2, 3, 4, 5, 6])
+@pytest.mark.parametrize("chi", [16, 32, 64])
+@pytest.mark.parametrize("split", ["0", "2"])
+def test_sweep_pt_split_groups(monkeypatch, N, chi, split):
+    """small batches: each trajectory over N^2 workgroups exchanging its state through global memory twice per
+    step (pt_split.hip), forced (2) and off (0), with MTOs of every kind, ragged windows and several systems"""
+    monkeypatch.setenv("PQD_SPLIT", split)
+    systems = [H.random_system(N, n_steps=30, seed=40 + k)[0] for k in range(3)]
+    grid = Grid(0.0, 0.1, 30)
+    n_traj = max(1, min(7, 256 // (N * N)))
+    tr = _traj(grid.n_steps, N, n_traj, seed=N + chi)
+    tr.system = np.array([k % 3 for k in range(n_traj)])
+    pt = ptmod.random_pt(N, chi, D=min(N * N, 9), n_slices=9, seed=chi + N, eps=0.15)
+    ops = [H.ketbra(N, 0, 0), H.ketbra(N, 1, 0), np.eye(N)]
+    rho0 = H.random_rho(N)
+    cmp_lists(engine.propagate(systems, grid, rho0, ops, tr, pt=pt),
+              oracle.propagate(systems, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
+
+
+def test_sweep_pt_split_full_c3_single_run(monkeypatch):
+    """C3 single run (one biexciton trajectory, chi = 64, 2000 steps): split groups vs the batched kernel"""
+    N, chi = 4, 64
+    sysd, grid = H.random_system(N, n_steps=2000, seed=7)
+    pt = ptmod.random_pt(N, chi, D=16, n_slices=300, seed=11, eps=0.1)
+    tr = Trajectories(np.array([0]), np.array([2000]))
+    ops = [H.ketbra(N, a, a) for a in range(N)]
+    rho0 = H.ketbra(N, 0, 0)
+    monkeypatch.setenv("PQD_SPLIT", "2")
+    a = engine.propagate(sysd, grid, rho0, ops, tr, pt=pt)
+    monkeypatch.setenv("PQD_SPLIT", "0")
+    b = engine.propagate(sysd, grid, rho0, ops, tr, pt=pt)
+    cmp_lists(a, b, 1e-11)
+
+
 def test_sweep_pt_many_trajectories_and_ragged_windows():
     N, chi = 4, 64
     sysd, grid = H.random_system(N, n_steps=40, seed=99)
