@@ -56,7 +56,7 @@ struct SplitLayout {
     static constexpr int KG = SP_NT / CHI;            // k groups of the row contraction
     static constexpr int KPER = CHI / KG;             // slice rows per thread
     static constexpr int RPT = (N2 + KG - 1) / KG;    // state rows per thread in the column phase
-    static constexpr int OPER = (N2 * N2 + SP_NT - 1) / SP_NT;  // operator elements per thread
+    static constexpr int OPER = (N2 * N2 + SP_NT - 1) / SP_NT;  // operator elements per thread (staging)
     static constexpr int LDS_STATE = 2 * N2 * CHI + N2 * N2 + N2 + SP_NT;  // complex elements
     static constexpr int LDS = (LDS_STATE * 16 > SP_LDS_FORCE) ? LDS_STATE * 16 : SP_LDS_FORCE;
 };
@@ -145,40 +145,32 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
     };
     auto has_event = [&](int n) { return ev_cur < ev_lim && p.ev[ev_cur].x == n; };
 
-    // slice row of PT(0) and the fused operator of step 1
-    double2 sreg[KPER], opreg[OPER];
+    // slice row of PT(0) and row g of the fused operator of step 1
+    double2 sreg[KPER], frow = c_zero();
     auto fetch_slice = [&](int n) {
         const double2* __restrict__ S = p.Q + ((size_t)p.sched[n] * p.D + p.gmap[g]) * CHI * CHI;
 #pragma unroll
         for (int j = 0; j < KPER; ++j) sreg[j] = gld(S + (size_t)(kq * KPER + j) * CHI + dcol);
     };
-    auto fetch_fused = [&](int n) {
-        const double2* __restrict__ M = Fg + (size_t)n * m2;
-#pragma unroll
-        for (int i = 0; i < OPER; ++i) {
-            const int e = tid + SP_NT * i;
-            opreg[i] = (e < m2) ? gld(M + e) : c_zero();
-        }
-    };
     if (n_end > 0) fetch_slice(0);
-    bool pre = false;  // opreg holds F(n) of the coming step
+    bool pre = false;  // frow holds F(n)[g][tid] of the coming step
     for (int n = 0;; ++n) {
         // ---- column phase
         const bool fz = p.fuse && n >= 1 && !has_event(n);
+        int rb;  // row g of the state the PT contracts
         if (fz) {
-            output(n, Wg + (size_t)n * p.n_out * N2);
-            if (n >= n_end) break;
+            // only row g of F(n) Q is needed here; Q itself stays for the deferred output(n) through W(n)
+            if (n >= n_end) { output(n, Wg + (size_t)n * p.n_out * N2); break; }
+            if (tid < N2) smem[OPO + tid] = pre ? frow : gld(Fg + (size_t)n * m2 + (size_t)g * N2 + tid);
             __syncthreads();
-            if (pre) {
+            if (tid < CHI) {
+                double2 acc = c_zero();
 #pragma unroll
-                for (int i = 0; i < OPER; ++i) {
-                    const int e = tid + SP_NT * i;
-                    if (e < m2) smem[OPO + e] = opreg[i];
-                }
-                apply_lds();
-            } else {
-                apply_global(Fg + (size_t)n * m2);
+                for (int b = 0; b < N2; ++b) c_fma(acc, smem[OPO + b], smem[qo + b * CHI + tid]);
+                smem[to + g * CHI + tid] = acc;
             }
+            __syncthreads();
+            rb = to + g * CHI;
         } else {
             if (n > 0) apply_global(Mg + (size_t)(2 * (n - 1) + 1) * m2);
             while (ev_cur < ev_lim) {  // applyBefore MTOs at n
@@ -196,11 +188,12 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
                 ++ev_cur;
             }
             apply_global(Mg + (size_t)(2 * n) * m2);
+            rb = qo + g * CHI;
         }
-        // ---- PT row g: y = Q[g][:] . S(n) -> exchange buffer (parity n & 1)
+        // ---- PT row g: y = row . S(n) -> exchange buffer (parity n & 1)
         double2 acc = c_zero();
 #pragma unroll
-        for (int j = 0; j < KPER; ++j) c_fma(acc, smem[qo + g * CHI + kq * KPER + j], sreg[j]);
+        for (int j = 0; j < KPER; ++j) c_fma(acc, smem[rb + kq * KPER + j], sreg[j]);
         smem[REDO + tid] = acc;
         __syncthreads();
         double2* Xn = Xt + (size_t)(n & 1) * E;
@@ -214,9 +207,10 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) __hip_atomic_fetch_add((gu32*)ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (fz) output(n, Wg + (size_t)n * p.n_out * N2);  // off the group's critical path (workgroup 0 only)
         if (n + 1 < n_end) fetch_slice(n + 1);
         pre = p.fuse && n + 1 < n_end && !has_event(n + 1);
-        if (pre) fetch_fused(n + 1);
+        if (pre && tid < N2) frow = gld(Fg + (size_t)(n + 1) * m2 + (size_t)g * N2 + tid);
         if (tid < 64) {
             const unsigned target = (unsigned)G * (unsigned)(n + 1);
             unsigned spins = 0;
