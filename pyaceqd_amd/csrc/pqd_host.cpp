@@ -530,14 +530,14 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess) n_cu = prop.multiProcessorCount;
     }
-    // latency path: a batch of at most split_max trajectories spreads each over N2 workgroups
-    // (PQD_SPLIT: 0 off, 1 auto, 2 whenever the device holds the groups)
+    // latency path: a batch whose trajectories fit one group of N2 workgroups each on the device runs
+    // each trajectory over N2 workgroups (pt_split.hip). Measured: 2.3-3.6x faster per step
+    // at N2 = 16 and 36; at N2 = 4 the batched kernel's single workgroup is as fast, so auto mode skips it.
+    // PQD_SPLIT: 0 off, 1 auto, 2 whenever the device holds the groups.
     {
         const char* e = getenv("PQD_SPLIT");
         const int mode = e ? atoi(e) : 1;
-        const int split_max = 8;
-        P->split = pt && mode != 0 && split_supported(N2, P->CHI, tr->n_traj, n_cu) &&
-                   (mode == 2 || tr->n_traj <= split_max);
+        P->split = pt && mode != 0 && split_supported(N2, P->CHI, tr->n_traj, n_cu) && (mode == 2 || N2 >= 9);
     }
     int BT = (sweep_max_bt(N2) >= 8 && tr->n_traj >= 8 * n_cu) ? 8 : 4;
     if (const char* e = getenv("PQD_BT")) BT = std::min(atoi(e) >= 8 ? 8 : 4, sweep_max_bt(N2));
