@@ -11,6 +11,12 @@
 // degree <= 18 whose remainder bound is below 2^-56 (the oracle always uses 18), then s squarings.
 // The N2 x N2 operands live in LDS; each of the 256 threads owns ceil(N2^2/256) output entries.
 #include "pqd_common.h"
+#include <algorithm>
+#include <cstdlib>
+
+// blocks per launch: 256-thread blocks keep the dispatch grid (work-items, 32 bits) below 2^32; larger
+// batches loop (grid-stride)
+constexpr long long FP_MAX_BLOCKS = 1LL << 22;
 
 namespace {
 
@@ -48,8 +54,11 @@ __global__ __launch_bounds__(256) void free_prop_kernel(FreePropParams p) {
     __shared__ int s_sh, s_deg;
 
     const int tid = threadIdx.x;
-    const int si = blockIdx.x / (2 * p.n_steps);
-    const int m = blockIdx.x - si * 2 * p.n_steps;
+    const long long nblk = (long long)p.n_sys * 2 * p.n_steps;
+    // grid-stride: the dispatch grid counts work-items in 32 bits, so a launch is capped (FP_MAX_BLOCKS)
+    for (long long blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    const int si = (int)(blk / (2 * p.n_steps));
+    const int m = (int)(blk - (long long)si * 2 * p.n_steps);
     const int n = m >> 1, h = m & 1;
     const FreePropSys sy = p.systems[si];
     const int nsub = p.n_sub > 0 ? p.n_sub : 1;
@@ -134,6 +143,79 @@ __global__ __launch_bounds__(256) void free_prop_kernel(FreePropParams p) {
     }
     double2* out = p.M + ((size_t)si * 2 * p.n_steps + m) * N2 * N2;
     for (int e = tid; e < N2 * N2; e += 256) out[e] = Acc[e];
+    __syncthreads();  // Acc is rewritten by the next matrix
+    }
+}
+
+// N2 = 4 (two-level system): a 4 x 4 matrix is 16 lanes, so a wave carries 4 matrices
+// and a 256-thread workgroup 16 — the general kernel would give each one a whole workgroup with 16 of
+// its 256 threads busy and a barrier per matmul. Lane (matrix, i, j) holds element (i, j) of A, P and
+// the accumulated product; products gather their row/column operands by lane shuffles inside the
+// 16-lane group (same matrix, so the same degree and squaring count: the group never diverges
+// internally). The arithmetic (sum orders included) is the general kernel's.
+__device__ __forceinline__ double2 c_shfl(double2 v, int src) {
+    return make_double2(__shfl(v.x, src), __shfl(v.y, src));
+}
+
+// C(i,j) = sum_k A(i,k) B(k,j) within the 16-lane group starting at lane gb
+__device__ __forceinline__ double2 grp_matmul4(double2 a, double2 b, int gb, int i, int j) {
+    double2 acc = c_zero();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c_fma(acc, c_shfl(a, gb + i * 4 + k), c_shfl(b, gb + k * 4 + j));
+    return acc;
+}
+
+__global__ __launch_bounds__(256) void free_prop4_kernel(FreePropParams p) {
+    const int tid = threadIdx.x;
+    const long long n_mat = (long long)p.n_sys * 2 * p.n_steps;
+    for (long long base = (long long)blockIdx.x * 16; base < n_mat; base += (long long)gridDim.x * 16) {
+    const long long mat = base + (tid >> 4);
+    const bool live = mat < n_mat;
+    const long long mc = live ? mat : n_mat - 1;  // dead lanes shadow the last matrix (no store)
+    const int si = (int)(mc / (2 * p.n_steps));
+    const int m = (int)(mc - (long long)si * 2 * p.n_steps);
+    const int n = m >> 1, h = m & 1;
+    const int lane = tid & 63, gb = lane & ~15, e = lane & 15, i = e >> 2, j = e & 3;
+    const FreePropSys sy = p.systems[si];
+    const int nsub = p.n_sub > 0 ? p.n_sub : 1;
+    const double w = 0.5 * p.dt / nsub;
+    double2 acc = c_zero();
+    for (int js = 0; js < nsub; ++js) {
+        const double t = p.ta + n * p.dt + h * 0.5 * p.dt + (js + 0.5) * w;
+        double2 v = sy.L0[e];
+        for (int c = 0; c < sy.n_chan && c < 4; ++c) {
+            const double2 f = sample_ch(sy, c, t);
+            c_fma(v, f, sy.S[(size_t)c * 16 + e]);
+            c_fma(v, c_conj(f), sy.T[(size_t)c * 16 + e]);
+        }
+        double2 a = c_scale(v, w);
+        // 1-norm: column sums in row order (as the general kernel), then the max over columns
+        double cs = 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { const double2 x = c_shfl(a, gb + r * 4 + j); cs += hypot(x.x, x.y); }
+        double norm = 0.0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) { const double x = __shfl(cs, gb + c); norm = x > norm ? x : norm; }
+        int e2 = 0;
+        frexp(norm / 0.5, &e2);
+        const int sh = e2 > 0 ? e2 : 0;
+        const double theta = ldexp(norm, -sh);
+        double rem = 0.5 * theta * theta;
+        int deg = 1;
+        while (deg < 18 && rem * 1.7 > 1.4e-17) { ++deg; rem *= theta / (deg + 1); }
+        a = c_scale(a, ldexp(1.0, -sh));
+        double2 pm = make_double2(a.x / (double)deg, a.y / (double)deg);
+        if (i == j) pm.x += 1.0;
+        for (int mm = deg - 1; mm >= 1; --mm) {
+            const double2 tv = grp_matmul4(a, pm, gb, i, j);
+            pm = make_double2(tv.x / (double)mm, tv.y / (double)mm);
+            if (i == j) pm.x += 1.0;
+        }
+        for (int q = 0; q < sh; ++q) pm = grp_matmul4(pm, pm, gb, i, j);
+        acc = (js == 0) ? pm : grp_matmul4(pm, acc, gb, i, j);
+    }
+    if (live) p.M[((size_t)si * 2 * p.n_steps + m) * 16 + e] = acc;
+    }
 }
 
 template <int N2>
@@ -146,9 +228,10 @@ hipError_t launch_fp(const FreePropParams& p, hipStream_t s) {
         if (e != hipSuccess) return e;
         attr = true;
     }
-    const int nblk = 2 * p.n_steps * p.n_sys;
+    const long long nblk = 2LL * p.n_steps * p.n_sys;
     if (nblk <= 0) return hipSuccess;
-    hipLaunchKernelGGL(free_prop_kernel<N2>, dim3(nblk), dim3(256), lds, s, p);
+    hipLaunchKernelGGL(free_prop_kernel<N2>, dim3((unsigned)std::min<long long>(nblk, FP_MAX_BLOCKS)), dim3(256), lds,
+                       s, p);
     return hipGetLastError();
 }
 
@@ -158,7 +241,9 @@ hipError_t launch_fp(const FreePropParams& p, hipStream_t s) {
 // before M_b(m-1) through W(m)[k] = ovec[k] . M_b(m-1) (a row vector per output operator).
 template <int N2>
 __global__ __launch_bounds__(256) void fuse_steps_kernel(FuseParams p) {
-    const int si = blockIdx.x / p.n_steps, m = blockIdx.x - si * p.n_steps + 1;  // m = 1..n_steps
+    const long long nblk = (long long)p.n_sys * p.n_steps;
+    for (long long blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    const int si = (int)(blk / p.n_steps), m = (int)(blk - (long long)si * p.n_steps) + 1;  // m = 1..n_steps
     const int tid = threadIdx.x;
     const double2* Mb = p.M + ((size_t)si * 2 * p.n_steps + 2 * (m - 1) + 1) * N2 * N2;
     if (m < p.n_steps) {
@@ -180,13 +265,15 @@ __global__ __launch_bounds__(256) void fuse_steps_kernel(FuseParams p) {
         for (int b = 0; b < N2; ++b) c_fma(acc, p.ovec[k * N2 + b], Mb[b * N2 + a]);
         W[e] = acc;
     }
+    }
 }
 
 template <int N2>
 hipError_t launch_fs(const FuseParams& p, hipStream_t s) {
-    const int nblk = p.n_sys * p.n_steps;
+    const long long nblk = (long long)p.n_sys * p.n_steps;
     if (nblk <= 0) return hipSuccess;
-    hipLaunchKernelGGL(fuse_steps_kernel<N2>, dim3(nblk), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(fuse_steps_kernel<N2>, dim3((unsigned)std::min<long long>(nblk, FP_MAX_BLOCKS)), dim3(256), 0,
+                       s, p);
     return hipGetLastError();
 }
 
@@ -204,6 +291,14 @@ hipError_t launch_fuse_steps(int N2, const FuseParams& p, hipStream_t s) {
 }
 
 hipError_t launch_free_prop(int N2, const FreePropParams& p, hipStream_t s) {
+    static const bool small4 = [] { const char* e = getenv("PQD_FP4"); return !e || atoi(e) != 0; }();
+    if (N2 == 4 && small4) {  // PQD_FP4=0: the general one-workgroup-per-matrix kernel (A/B)
+        const long long n_mat = (long long)p.n_sys * 2 * p.n_steps;
+        if (n_mat <= 0) return hipSuccess;
+        hipLaunchKernelGGL(free_prop4_kernel, dim3((unsigned)std::min<long long>((n_mat + 15) / 16, FP_MAX_BLOCKS)),
+                           dim3(256), 0, s, p);
+        return hipGetLastError();
+    }
     switch (N2) {
         case 4: return launch_fp<4>(p, s);
         case 9: return launch_fp<9>(p, s);

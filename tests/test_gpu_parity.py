@@ -82,7 +82,7 @@ def test_sweep_pt(N, chi):
 @pytest.mark.parametrize("chi", [16, 32, 64])
 @pytest.mark.parametrize("split", ["0", "2"])
 def test_sweep_pt_split_groups(monkeypatch, N, chi, split):
-    """small batches: each trajectory over N^2 workgroups exchanging its state through global memory twice per
+    """small batches: each trajectory over N^2 workgroups gathering its state through global memory once per
     step (pt_split.hip), forced (2) and off (0), with MTOs of every kind, ragged windows and several systems"""
     monkeypatch.setenv("PQD_SPLIT", split)
     systems = [H.random_system(N, n_steps=30, seed=40 + k)[0] for k in range(3)]
@@ -110,6 +110,23 @@ def test_sweep_pt_split_full_c3_single_run(monkeypatch):
     monkeypatch.setenv("PQD_SPLIT", "0")
     b = engine.propagate(sysd, grid, rho0, ops, tr, pt=pt)
     cmp_lists(a, b, 1e-11)
+
+
+@pytest.mark.parametrize("fp4", ["0", "1"])
+def test_free_propagators_beyond_32bit_dispatch(monkeypatch, fp4):
+    """a scan whose free propagators need more than 2^32 work-items in one-workgroup-per-matrix form
+    (1700 systems x 2 x 5000 half steps = 17M matrices x 256 threads): the kernels loop over a capped grid.
+    All systems are identical, so every trajectory's last outputs must agree exactly with the first's."""
+    monkeypatch.setenv("PQD_FP4", fp4)
+    N, n_sys, n_steps = 2, 1700, 5000
+    sysd, grid = H.random_system(N, n_chan=1, n_lind=1, seed=5, n_steps=n_steps)
+    tr = Trajectories(np.full(n_sys, n_steps - 1), np.full(n_sys, n_steps))
+    tr.system = np.arange(n_sys)
+    out = engine.propagate([sysd] * n_sys, grid, H.ketbra(N, 0, 0), [H.ketbra(N, 1, 1), H.ketbra(N, 0, 1)], tr)
+    ref = out[0]
+    assert np.all(np.isfinite(ref)) and np.abs(ref).max() > 0
+    for k in (1, n_sys // 2, n_sys - 1):
+        np.testing.assert_array_equal(out[k], ref)
 
 
 def test_sweep_pt_many_trajectories_and_ragged_windows():
@@ -642,7 +659,11 @@ def test_tpe_rotation_scan_vs_oracle(monkeypatch, tmp_path):
 # --------------------------------------------------------------------------------- time-bin two-photon states
 def test_twophoton_timebin_tl_paths_vs_reference_golden(golden_dir, tmp_path):
     """TwoPhotonTimebinNew time-local-map paths (four_time_8op / four_time kernels, utils.fast_propagate) vs the
-    reference class with the reference Fortran on the same synthetic maps (tests/golden/pyref_twophoton.npz)"""
+    reference class with the reference Fortran on the same synthetic maps (tests/golden/pyref_twophoton.npz).
+    The time-local maps come from the GPU Jacobi-SVD pinv (tools.calc_tl_dynmap_pseudo), the golden from LAPACK's
+    SVD inside numpy's pinv: both are backward stable, and on these damped maps they agree to cond * eps
+    (measured 4.8e-10 relative on the density matrix), hence 2e-9 here instead of the 1e-11 of pure sweeps."""
+    tol = 2e-9
     from pyaceqd_amd.pulses import ChirpedPulse
     from pyaceqd_amd.timebin.twophoton_new import TwoPhotonTimebinNew
     from tests.fake_system import fake_system_dm
@@ -652,14 +673,14 @@ def test_twophoton_timebin_tl_paths_vs_reference_golden(golden_dir, tmp_path):
     tl = TwoPhotonTimebinNew(fake_system_dm, "|0><1|_4", "|1><0|_4", "|1><3|_4", "|3><1|_4", *ps, options=opts,
                              dt=0.1, dim=4, tb=12, dt_small=0.5, n_tbig=2, gaussian_t=6)
     c, rho, _ = tl.calc_densitymatrix_tl(reduced=False)
-    assert rel(rho, z["tl_rho"]) < 1e-11
-    assert rel(tl.eell_tl_f()[3], z["tl_eell_f"]) < 1e-11
+    assert rel(rho, z["tl_rho"]) < tol
+    assert rel(tl.eell_tl_f()[3], z["tl_eell_f"]) < tol
     t, r = tl.dynamics_tl()
-    assert rel(r, z["tl_dyn_rho"]) < 1e-11
+    assert rel(r, z["tl_dyn_rho"]) < tol
     t, r = tl.dynamics_tl_t1()
-    assert rel(r, z["tl_dyn1_rho"]) < 1e-11
+    assert rel(r, z["tl_dyn1_rho"]) < tol
     ft = tl.four_time_tl(tl.sigma_bdag, tl.sigma_xdag, tl.sigma_b, tl.sigma_x)
-    assert rel(ft[3], z["tl_ft_table"]) < 1e-11
+    assert rel(ft[3], z["tl_ft_table"]) < tol
 
 
 def test_twophoton_timebin_biexciton_vs_oracle(monkeypatch, tmp_path):
