@@ -661,9 +661,10 @@ def test_twophoton_timebin_tl_paths_vs_reference_golden(golden_dir, tmp_path):
     """TwoPhotonTimebinNew time-local-map paths (four_time_8op / four_time kernels, utils.fast_propagate) vs the
     reference class with the reference Fortran on the same synthetic maps (tests/golden/pyref_twophoton.npz).
     The time-local maps come from the GPU Jacobi-SVD pinv (tools.calc_tl_dynmap_pseudo), the golden from LAPACK's
-    SVD inside numpy's pinv: both are backward stable, and on these damped maps they agree to cond * eps
-    (measured 4.8e-10 relative on the density matrix), hence 2e-9 here instead of the 1e-11 of pure sweeps."""
-    tol = 2e-9
+    SVD inside numpy's pinv. These damped cumulative maps reach cond = 3.8e10; against a 40-digit inverse both
+    pinvs are off by ~3e-7 at the map level (LAPACK 2.7e-7, Jacobi 3.7e-7), and the two differ from each other by
+    5e-9 relative in the outputs below. Hence the north-star no-phonon bar, 1e-8, instead of the sweeps' 1e-11."""
+    tol = 1e-8
     from pyaceqd_amd.pulses import ChirpedPulse
     from pyaceqd_amd.timebin.twophoton_new import TwoPhotonTimebinNew
     from tests.fake_system import fake_system_dm
