@@ -34,6 +34,35 @@ __device__ __forceinline__ double2 sample_ch(const FreePropSys& p, int c, double
 
 template <int N2>
 __device__ __forceinline__ void lds_matmul(const double2* A, const double2* B, double2* C, int tid) {
+    if constexpr (N2 == 36) {
+        // 3 x 3 register blocks on 144 threads: one LDS read feeds 3 complex MACs instead of 1/2 (the 1x1 form is
+        // LDS-bandwidth bound, ≈16 TF/s chip-wide); every element keeps the k = 0..N2-1 summation order
+        if (tid < 144) {
+            const int r0 = 3 * (tid / 12), c0 = 3 * (tid % 12);
+            double2 acc[3][3];
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) acc[r][c] = c_zero();
+#pragma unroll 4
+            for (int k = 0; k < N2; ++k) {
+                double2 a[3], b[3];
+#pragma unroll
+                for (int r = 0; r < 3; ++r) a[r] = A[(r0 + r) * N2 + k];
+#pragma unroll
+                for (int c = 0; c < 3; ++c) b[c] = B[k * N2 + c0 + c];
+#pragma unroll
+                for (int r = 0; r < 3; ++r)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) c_fma(acc[r][c], a[r], b[c]);
+            }
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) C[(r0 + r) * N2 + c0 + c] = acc[r][c];
+        }
+        return;
+    }
     for (int e = tid; e < N2 * N2; e += 256) {
         const int i = e / N2, j = e - i * N2;
         double2 acc = c_zero();
@@ -132,7 +161,9 @@ __global__ __launch_bounds__(256) void free_prop_kernel(FreePropParams p) {
             for (int e = tid; e < N2 * N2; e += 256) P[e] = T[e];
             __syncthreads();
         }
-        if (j == 0) {
+        if (nsub == 1) {
+            // single factor: P is the propagator (no Acc buffer allocated, so two workgroups fit a CU at N2 = 36)
+        } else if (j == 0) {
             for (int e = tid; e < N2 * N2; e += 256) Acc[e] = P[e];
         } else {
             lds_matmul<N2>(P, Acc, T, tid);
@@ -142,7 +173,8 @@ __global__ __launch_bounds__(256) void free_prop_kernel(FreePropParams p) {
         __syncthreads();
     }
     double2* out = p.M + ((size_t)si * 2 * p.n_steps + m) * N2 * N2;
-    for (int e = tid; e < N2 * N2; e += 256) out[e] = Acc[e];
+    const double2* res = (nsub == 1) ? P : Acc;
+    for (int e = tid; e < N2 * N2; e += 256) out[e] = res[e];
     __syncthreads();  // Acc is rewritten by the next matrix
     }
 }
@@ -230,8 +262,10 @@ hipError_t launch_fp(const FreePropParams& p, hipStream_t s) {
     }
     const long long nblk = 2LL * p.n_steps * p.n_sys;
     if (nblk <= 0) return hipSuccess;
-    hipLaunchKernelGGL(free_prop_kernel<N2>, dim3((unsigned)std::min<long long>(nblk, FP_MAX_BLOCKS)), dim3(256), lds,
-                       s, p);
+    // A, P, T (+ Acc only for n_sub > 1): at N2 = 36, 62 KiB instead of 83 KiB lets two workgroups share a CU
+    const size_t lds_run = (p.n_sub > 1 ? 4ull : 3ull) * N2 * N2 * sizeof(double2);
+    hipLaunchKernelGGL(free_prop_kernel<N2>, dim3((unsigned)std::min<long long>(nblk, FP_MAX_BLOCKS)), dim3(256),
+                       lds_run, s, p);
     return hipGetLastError();
 }
 
