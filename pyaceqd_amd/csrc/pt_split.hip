@@ -21,6 +21,7 @@
 // output(n), applyAfter MTOs at n, M_a(n), PT(n); steps without MTOs use F(n) and read the outputs
 // through W(n) = ovec M_b(n-1), as the batched kernel does.
 #include "pqd_common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -45,6 +46,19 @@ __device__ __forceinline__ double2 gld(const double2* p) {
     return make_double2(q[0], q[1]);
 }
 
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+
+// 16-B sc1 payload accesses through a buffer descriptor (aux 16 = sc1): one dwordx4 per complex element
+__device__ __forceinline__ void st_sc1_b128(__amdgpu_buffer_rsrc_t r, int off, double2 v) {
+    v4u32 w;
+    w.x = __double2loint(v.x); w.y = __double2hiint(v.x); w.z = __double2loint(v.y); w.w = __double2hiint(v.y);
+    __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, 16);
+}
+__device__ __forceinline__ double2 ld_sc1_b128(__amdgpu_buffer_rsrc_t r, int off) {
+    const v4u32 w = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
+    return make_double2(__hiloint2double(w.y, w.x), __hiloint2double(w.w, w.z));
+}
+
 __device__ __forceinline__ double2 ld_sc1(const double2* p) {
     const unsigned long long x = __hip_atomic_load((gu64*)&p->x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long y = __hip_atomic_load((gu64*)&p->y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -61,7 +75,7 @@ struct SplitLayout {
     static constexpr int LDS = (LDS_STATE * 16 > SP_LDS_FORCE) ? LDS_STATE * 16 : SP_LDS_FORCE;
 };
 
-template <int N2, int CHI>
+template <int N2, int CHI, bool B128>
 __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2* __restrict__ X,
                                                          unsigned* __restrict__ cnt, unsigned* __restrict__ err) {
     using L = SplitLayout<N2, CHI>;
@@ -82,6 +96,8 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
     const double2* __restrict__ Fg = p.F + (size_t)sy * p.f_stride;
     const double2* __restrict__ Wg = p.W + (size_t)sy * p.w_stride;
     double2* __restrict__ Xt = X + (size_t)t * 2 * E;
+    // descriptor over this trajectory's two exchange slots, from workgroup-uniform values only
+    const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(Xt, 0, 2 * E * 16, 0x00020000);
     unsigned* ct = cnt + (size_t)t * 32;  // one 128-B line per group counter
     const int n_end = we;
     constexpr int m2 = N2 * N2;
@@ -201,7 +217,8 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
             double2 y = smem[REDO + tid];
 #pragma unroll
             for (int q = 1; q < KG; ++q) y = c_add(y, smem[REDO + q * CHI + tid]);
-            st_sc1(Xn + (size_t)g * CHI + tid, y);
+            if (B128) st_sc1_b128(rX, (int)(((size_t)(n & 1) * E + (size_t)g * CHI + tid) * 16), y);
+            else st_sc1(Xn + (size_t)g * CHI + tid, y);
         }
         // ---- arrive, prefetch the next step's slice row and fused operator, then wait for the group
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -227,24 +244,36 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         __syncthreads();
         if (s_abort) return;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: payload loads are sc1
-        for (int e = tid; e < E; e += SP_NT) smem[qo + e] = ld_sc1(Xn + e);
+        if (B128) {
+            for (int e = tid; e < E; e += SP_NT) smem[qo + e] = ld_sc1_b128(rX, (int)(((size_t)(n & 1) * E + e) * 16));
+        } else {
+            for (int e = tid; e < E; e += SP_NT) smem[qo + e] = ld_sc1(Xn + e);
+        }
         __syncthreads();
     }
 }
 
-template <int N2, int CHI>
-hipError_t launch_split_t(int n_traj, const SweepParams& p, double2* X, unsigned* cnt, unsigned* err, hipStream_t s) {
+template <int N2, int CHI, bool B128>
+hipError_t launch_split_tb(int n_traj, const SweepParams& p, double2* X, unsigned* cnt, unsigned* err, hipStream_t s) {
     using L = SplitLayout<N2, CHI>;
     static_assert(L::LDS <= 160 * 1024, "LDS budget");
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)pt_split_kernel<N2, CHI>,
+        hipError_t e = hipFuncSetAttribute((const void*)pt_split_kernel<N2, CHI, B128>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::LDS);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((pt_split_kernel<N2, CHI>), dim3(n_traj * N2), dim3(SP_NT), L::LDS, s, p, X, cnt, err);
+    hipLaunchKernelGGL((pt_split_kernel<N2, CHI, B128>), dim3(n_traj * N2), dim3(SP_NT), L::LDS, s, p, X, cnt, err);
     return hipGetLastError();
+}
+
+template <int N2, int CHI>
+hipError_t launch_split_t(int n_traj, const SweepParams& p, double2* X, unsigned* cnt, unsigned* err, hipStream_t s) {
+    // PQD_SPLIT_B128=1: 16-B sc1 buffer accesses for the exchange (A/B switch; 0 = two 8-B atomics per element)
+    static const bool b128 = [] { const char* e = getenv("PQD_SPLIT_B128"); return e && atoi(e) != 0; }();
+    return b128 ? launch_split_tb<N2, CHI, true>(n_traj, p, X, cnt, err, s)
+                : launch_split_tb<N2, CHI, false>(n_traj, p, X, cnt, err, s);
 }
 
 template <int N2>
