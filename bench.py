@@ -233,6 +233,24 @@ def main():
                      "hbm_algorithmic_GBs": bytes_per_launch(grid.n_steps, 410, args.chi, n_traj=n_traj,
                                                              executed_steps=executed) / (ms_sweep * 1e-3) / 1e9},
     }
+    if rank == 0 and world == 1:
+        # the reference's single-run case (one trajectory of the same model, chi and length; outside the timed
+        # region): a latency figure, carried by N2 split workgroups
+        s_sys, s_grid, s_pt, s_rho0, s_ops, s_tr = build_workload(1, args.n_tau, args.chi, scan=1,
+                                                                  dictionary=bool(args.pt_dict))
+        sp = engine.Plan(s_sys, s_grid, s_rho0, s_ops, s_tr, pt=s_pt, ctx=ctx)
+        sp.execute()
+        sp.synchronize()
+        sp.timing(reset=True)
+        for _ in range(3):
+            sp.execute()
+        sp.synchronize()
+        _, s_ms, _ = sp.timing(reset=True)
+        line["single_run"] = {"workload": f"one biexciton G2 trajectory, chi={args.chi}, {args.n_tau} steps",
+                              "sweep_ms": s_ms, "us_per_step": s_ms * 1e3 / (args.n_tau + 1),
+                              "traj_steps_per_s": (args.n_tau + 1) / (s_ms * 1e-3),
+                              "path": "split groups (PQD_SPLIT)" if os.environ.get("PQD_SPLIT", "1") != "0"
+                              else "batched kernel"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.chi, args.cpu_seconds)
     if rank == 0:
