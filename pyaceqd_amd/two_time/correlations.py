@@ -110,7 +110,24 @@ def five_op_two_time(system, t_axis, *pulses, opA="|1><0|_2", opB="|1><0|_2", op
                          workers=workers, n_mto=2, t_start=t_start)
 
 
-def _tl_sweep(system, t_axis, pulses, t_mem, ops, tau_max, dt, rho0, options, use_dm, mtos_dyn):
+def _tl_sweep(system, t_axis, pulses, t_mem, ops, tau_max, dt, rho0, options, use_dm, fortran_only, mtos_dyn,
+              stationary_ops):
+    """Shared body of tl_two_op_two_time / tl_three_op_two_time (correlations.py:450-615, 696-863).
+
+    ops = (A, B, C): G(t, 0) = Tr(A B C rho(t)), rho -> C rho A at t, G(t, tau) = Tr(B rho(t + tau)).
+    use_dm, fortran_only=True  -> the reference's Fortran call (:781-782): calc_onetime_parallel on the GPU, which
+                                  reads the row-major vec(rho) column-major (it works with rho^T, SURVEY §8a);
+    use_dm, fortran_only=False -> the reference's row-major Python loop (:786-838: trunk `while _t[j] < t`,
+                                  Tr(ABC rho), C rho A, propagate_tau from map j, Tr(B rho_tau)). The same
+                                  calc_onetime_parallel kernel computes it exactly when handed (C^T, B^T, A^T): the
+                                  column-major view of vec(R) is R^T, Tr(C^T B^T A^T R^T) = Tr(A B C R), the MTO gives
+                                  A^T R^T C^T = (C R A)^T and Tr(B^T X^T) = Tr(B X). One launch for all t instead of one
+                                  propagate_tau per t.
+    not use_dm                 -> the stationary time-local map of a 0 .. 4 t_mem dynamical-map run with the MTOs at
+                                  2 t_mem (:743-750, :840-860), with `stationary_ops` = (A', B') giving
+                                  G(t, 0) = Tr(A' B' rho), rho -> B' rho, G(t, tau) = Tr(A' rho_tau) as the reference
+                                  writes it (for the three-op function that is its two-op formula, :856-860).
+    """
     if not t_axis[0] == 0:
         raise ValueError("t_axis must start at 0.")
     opA_mat, opB_mat, opC_mat = ops
@@ -123,46 +140,84 @@ def _tl_sweep(system, t_axis, pulses, t_mem, ops, tau_max, dt, rho0, options, us
         _t = np.round(np.real(result[0]), 6)
         dm_tl = calc_tl_dynmap_pseudo(dm, _t)
         dm_tl_f = np.asfortranarray(dm_tl.transpose(1, 2, 0))
-        G = propagate_tau_module.calc_onetime_parallel(dm_tl_f, rho0.reshape(dim ** 2), n_tau, dim, opA_mat, opB_mat,
-                                                       opC_mat, _t, t_axis)
-        return t_axis, tau, G
+        if fortran_only:
+            a, b, c = opA_mat, opB_mat, opC_mat
+        else:
+            a, b, c = opC_mat.T, opB_mat.T, opA_mat.T
+        G = propagate_tau_module.calc_onetime_parallel(dm_tl_f, np.asarray(rho0).reshape(dim ** 2), n_tau, dim, a, b,
+                                                       c, _t, t_axis)
+        return t_axis, tau, np.ascontiguousarray(G)
     result, dm = system(0, 4 * t_mem, *pulses, dt=dt, rho0=rho0, multitime_op=mtos_dyn, calc_dynmap=True, **options)
     _t = np.round(np.real(result[0]), 6)
     dm_tl = calc_tl_dynmap_pseudo(dm, _t)
     tl_map, _ = extract_dms(dm_tl, _t, t_mem, [2 * t_mem])
+    G = np.zeros((len(t_axis), len(tau)), dtype=complex)
     if options.get("phonons", False):
         print("phonons not implemented yet")
-        return t_axis, tau, np.zeros((len(t_axis), len(tau)), dtype=complex)
-    G = np.zeros((len(t_axis), len(tau)), dtype=complex)
-    rho_t = rho0.copy().reshape(dim ** 2)
+        return t_axis, tau, G
+    sA, sB = stationary_ops
+    rho_t = np.asarray(rho0, dtype=complex).copy().reshape(dim ** 2)
     for i, t in enumerate(t_axis):
         n_steps = 0 if i == 0 else int((t - t_axis[i - 1]) / dt)
         rho_t = np.linalg.matrix_power(tl_map, n_steps) @ rho_t
         R = rho_t.reshape(dim, dim)
-        G[i, 0] = np.trace(opA_mat @ opB_mat @ opC_mat @ R)
-        rho_m = opC_mat @ R @ opA_mat
-        rho_tau = tl_pad_stationary_nsteps(tl_map, n_tau, rho_m)
-        G[i, 1:] = np.trace(opB_mat @ rho_tau, axis1=1, axis2=2)
+        G[i, 0] = np.trace(sA @ sB @ R)
+        rho_tau = tl_pad_stationary_nsteps(tl_map, n_tau, sB @ R)
+        G[i, 1:] = np.trace(sA @ rho_tau, axis1=1, axis2=2)
     return t_axis, tau, G
 
 
 def tl_two_op_two_time(system, t_axis, *pulses, t_mem=10, opA="|1><0|_2", opB="|0><1|_2", tau_max=500, dt=0.1,
                        rho0=np.array([[1, 0], [0, 0]], dtype=complex), options={"lindblad": True, "phonons": False},
                        debug=False, workers=15, use_dm=False, fortran_only=False):
-    """<A(t + tau) B(t)> from dynamical maps (correlations.py:450-615; use_dm -> GPU map-chain sweep)"""
+    """<A(t + tau) B(t)> from dynamical maps (correlations.py:450-615; use_dm -> GPU map-chain sweep, either
+    convention of `fortran_only`)"""
     A, B = op_to_matrix(opA), op_to_matrix(opB)
     I = np.identity(A.shape[0], dtype=complex)
     mto = {"operator": opB, "applyFrom": "_left", "applyBefore": "false", "time": 2 * t_mem}
-    # <A(t+tau) B(t)> = Tr(A E(tau) [B rho(t)]): opA -> identity on the right, opB -> A, opC -> B
-    return _tl_sweep(system, t_axis, pulses, t_mem, (I, A, B), tau_max, dt, rho0, options, use_dm, [mto])
+    # <A(t+tau) B(t)> = Tr(A E(tau) [B rho(t)]): the reference passes (identity, A, B) as (opA, opB, opC) (:534)
+    return _tl_sweep(system, t_axis, pulses, t_mem, (I, A, B), tau_max, dt, rho0, options, use_dm, fortran_only,
+                     [mto], (A, B))
 
 
 def tl_three_op_two_time(system, t_axis, *pulses, t_mem=10, opA="|1><0|_2", opB="|1><1|_2", opC="|0><1|_2",
                          tau_max=500, dt=0.1, rho0=np.array([[1, 0], [0, 0]], dtype=complex),
                          options={"lindblad": True, "phonons": False}, debug=False, workers=15, use_dm=False,
-                         fortran_only=False):
-    """<A(t) B(t + tau) C(t)> from dynamical maps (correlations.py:696-863)"""
+                         fortran_only=False, three_op_stationary=False):
+    """<A(t) B(t + tau) C(t)> from dynamical maps (correlations.py:696-863).
+
+    Without use_dm the reference evaluates its TWO-op formula here, ignoring opC: G(t, 0) = Tr(A B rho),
+    rho -> B rho, G(t, tau) = Tr(A rho_tau) (:856-860); that is reproduced by default (pinned by
+    tests/golden/pyref_correlations.npz). `three_op_stationary=True` (not in the reference) evaluates the three-op
+    correlation on the stationary map instead: Tr(A B C rho), rho -> C rho A, Tr(B rho_tau)."""
     A, B, Cm = op_to_matrix(opA), op_to_matrix(opB), op_to_matrix(opC)
     mto = {"operator": opC, "applyFrom": "_left", "applyBefore": "false", "time": 2 * t_mem}
     mto2 = {"operator": opA, "applyFrom": "_right", "applyBefore": "false", "time": 2 * t_mem}
-    return _tl_sweep(system, t_axis, pulses, t_mem, (A, B, Cm), tau_max, dt, rho0, options, use_dm, [mto, mto2])
+    if three_op_stationary:
+        if use_dm:
+            raise ValueError("three_op_stationary applies to the stationary-map branch (use_dm=False) only")
+        return _tl_stationary_three_op(system, t_axis, pulses, t_mem, (A, B, Cm), tau_max, dt, rho0, options,
+                                       [mto, mto2])
+    return _tl_sweep(system, t_axis, pulses, t_mem, (A, B, Cm), tau_max, dt, rho0, options, use_dm, fortran_only,
+                     [mto, mto2], (A, B))
+
+
+def _tl_stationary_three_op(system, t_axis, pulses, t_mem, ops, tau_max, dt, rho0, options, mtos_dyn):
+    """opt-in three-op form of the stationary-map branch (see tl_three_op_two_time)"""
+    A, B, Cm = ops
+    dim = len(rho0[0])
+    n_tau = int(tau_max / dt)
+    tau = np.linspace(0, tau_max, n_tau + 1)
+    result, dm = system(0, 4 * t_mem, *pulses, dt=dt, rho0=rho0, multitime_op=mtos_dyn, calc_dynmap=True, **options)
+    _t = np.round(np.real(result[0]), 6)
+    tl_map, _ = extract_dms(calc_tl_dynmap_pseudo(dm, _t), _t, t_mem, [2 * t_mem])
+    G = np.zeros((len(t_axis), len(tau)), dtype=complex)
+    rho_t = np.asarray(rho0, dtype=complex).copy().reshape(dim ** 2)
+    for i, t in enumerate(t_axis):
+        n_steps = 0 if i == 0 else int((t - t_axis[i - 1]) / dt)
+        rho_t = np.linalg.matrix_power(tl_map, n_steps) @ rho_t
+        R = rho_t.reshape(dim, dim)
+        G[i, 0] = np.trace(A @ B @ Cm @ R)
+        rho_tau = tl_pad_stationary_nsteps(tl_map, n_tau, Cm @ R @ A)
+        G[i, 1:] = np.trace(B @ rho_tau, axis1=1, axis2=2)
+    return t_axis, tau, G

@@ -249,6 +249,122 @@ def _ref_with_fortran_module():
     sys.modules["pyaceqd.two_time.propagate_tau_module"] = ptm
 
 
+def _ref_correlations():
+    """Import the reference's own pyaceqd/two_time/correlations.py. Its module-level import chain (correlations.py:6
+    -> two_level_system/tls.py -> general_system.py:14) reaches the absent ACEutils pybind module; an empty placeholder
+    (every imported name None, nothing callable: SURVEY.md §4.3) satisfies that import. The model callables passed to
+    the reference functions are tests/fake_system.py or our own lowering on the CPU oracle (below), and
+    `propagate_tau_module` is the reference's OWN Fortran (oracle/fref.py)."""
+    import types
+    sys.path.insert(0, REF_ROOT)
+    for mod in ("pyaceqd.two_time.correlations", "pyaceqd.two_level_system.tls"):
+        if mod in sys.modules and getattr(sys.modules[mod], "__file__", None) is None:
+            del sys.modules[mod]  # placeholders left by _ref_with_fortran_module
+    if "ACEutils" not in sys.modules:
+        ace = types.ModuleType("ACEutils")
+        for n in ("Parameters", "FreePropagator", "ProcessTensors", "InitialState", "OutputPrinter", "TimeGrid",
+                  "Simulation", "read_outfile", "DynamicalMap"):
+            setattr(ace, n, None)
+        sys.modules["ACEutils"] = ace
+    ptm = types.ModuleType("pyaceqd.two_time.propagate_tau_module")
+    for name in ("propagate_tau", "calc_onetime_parallel", "calc_onetime_parallel_block", "calc_twotime_phonon_block"):
+        setattr(ptm, name, getattr(fref, name))
+    sys.modules["pyaceqd.two_time.propagate_tau_module"] = ptm
+    import pyaceqd.two_time as pkg  # noqa: E402
+    pkg.propagate_tau_module = ptm
+    from pyaceqd.two_time import correlations  # noqa: E402
+    return correlations
+
+
+def gen_correlations():
+    """two_time/correlations.py: the REFERENCE one-/two-time drivers (`_ops_one_time`, `_ops_two_time` and the four
+    public wrappers, the time-local-map `tl_two_op_two_time` / `tl_three_op_two_time` in all three branches
+    use_dm x fortran_only) on the deterministic tests/fake_system.py models; ours run the same calls in
+    tests/test_callers_golden.py (CPU) and tests/test_gpu_parity.py (map-chain sweeps on the GPU)."""
+    import io
+    import contextlib
+    import warnings
+    warnings.simplefilter("ignore")
+    R = _ref_correlations()
+    from pyaceqd.pulses import ChirpedPulse  # noqa: E402
+    from tests.fake_system import fake_system, fake_system_dm  # noqa: E402
+    p = ChirpedPulse(tau_0=1.0, e_start=0, e0=1.5, t0=2)
+    opts = lambda **k: dict({"lindblad": True, "phonons": False}, **k)  # noqa: E731
+    t_axis = np.round(np.arange(7) * 0.3, 6)
+    out = {"t_axis": t_axis}
+    quiet = contextlib.redirect_stdout(io.StringIO())
+    with quiet, contextlib.redirect_stderr(io.StringIO()):
+        tau, G = R.two_op_one_time(fake_system, p, opA="|1><0|_2", opB="|0><1|_2", t0=-2, t_MTO=1.0, tend=4, dt=0.1,
+                                   options=opts())
+        out.update(ot2_tau=tau, ot2_G=G)
+        tau, G = R.three_op_one_time(fake_system, p, t0=-2, t_MTO=1.0, tend=4, dt=0.1, options=opts())
+        out.update(ot3_tau=tau, ot3_G=G)
+        for tag, fn, kw in (("tt2", R.two_op_two_time, {}),
+                            ("tt3", R.three_op_two_time, {}),
+                            ("tt3s", R.three_op_two_time, {"t_start": -1.0}),
+                            ("tt5", R.five_op_two_time, {"t_start": -1.0})):
+            t1, t2, G = fn(fake_system, t_axis, p, tau_max=2.0, dt=0.1, options=opts(), workers=2, **kw)
+            out.update({f"{tag}_t1": t1, f"{tag}_t2": t2, f"{tag}_G": G})
+        rho2 = np.array([[0.8, 0.1 - 0.05j], [0.1 + 0.05j, 0.2]], dtype=complex)
+        for tag, fn, kw in (("tl2", R.tl_two_op_two_time, {}),
+                            ("tl3", R.tl_three_op_two_time, {"opC": "|0><1|_2"})):
+            for use_dm, fo in ((False, False), (True, False), (True, True)):
+                t1, t2, G = fn(fake_system_dm, t_axis, p, t_mem=1.0, tau_max=2.0, dt=0.1, rho0=rho2,
+                               options=opts(), use_dm=use_dm, fortran_only=fo, **kw)
+                out[f"{tag}_dm{int(use_dm)}_f{int(fo)}_G"] = G
+                out[f"{tag}_t2"] = t2
+        # a non-hermitian-pair operator set on a 4-level fake model (the fortran_only view differs from the
+        # row-major one there: both are pinned)
+        rho4 = np.diag([0.5, 0.2, 0.2, 0.1]).astype(complex)
+        rho4[0, 3] = rho4[3, 0] = 0.05
+        for use_dm, fo in ((False, False), (True, False), (True, True)):
+            t1, t2, G = R.tl_three_op_two_time(fake_system_dm, t_axis, p, t_mem=1.0, opA="|1><0|_4", opB="|2><1|_4",
+                                               opC="|3><1|_4", tau_max=1.5, dt=0.1, rho0=rho4,
+                                               options=opts(fake_dim=4), use_dm=use_dm, fortran_only=fo)
+            out[f"tl3d4_dm{int(use_dm)}_f{int(fo)}_G"] = G
+    np.savez_compressed(os.path.join(HERE, "pyref_correlations.npz"), **out)
+
+
+def gen_twotime_anchor():
+    """Reference-anchored two-time semantics of the PT path: exact no-phonon dynamical maps of a
+    driven, decaying biexciton (our lowering of `biexciton`, propagated by the CPU oracle: dm[i] = E(t_{i+1}, 0)) are
+    fed to the REFERENCE tl_three_op_two_time / tl_two_op_two_time (use_dm=True; time-localised by the reference's
+    calc_tl_dynmap_pseudo, swept by the reference's own Fortran or its row-major Python path). The GPU test runs our
+    trajectory sweep `three_op_two_time` / `two_op_two_time` (MTOs at t1 inside the PT kernel) on the same model and
+    must reproduce these G within 1e-10."""
+    import io
+    import contextlib
+    import warnings
+    warnings.simplefilter("ignore")
+    R = _ref_correlations()
+    from oracle import oracle
+    import pyaceqd_amd._lib as L
+    from pyaceqd_amd.general_system import general_system as gs
+    from pyaceqd_amd.four_level_system.linear import biexciton
+    from pyaceqd_amd.pulses import ChirpedPulse
+    L.context = lambda device=None: None  # noqa: E731  (no device in the build container)
+    gs.propagate = lambda system, grid, rho0, out_ops, traj, pt=None, ctx=None: oracle.propagate(  # noqa: E731
+        system, grid, rho0, out_ops, traj, pt=pt, nthreads=8)
+    p = ChirpedPulse(tau_0=1.0, e_start=-2.0, e0=1.3, t0=1.5, polar_x=0.8)
+    t_axis = np.round(np.arange(8) * 0.5, 6)
+    rho0 = np.zeros((4, 4), dtype=complex)
+    rho0[0, 0] = 1.0
+    opts = lambda: {"lindblad": True, "phonons": False, "delta_b": 4.0, "delta_xy": 0.03}  # noqa: E731
+    out = {"t_axis": t_axis, "tau_max": 4.0, "dt": 0.1}
+    with contextlib.redirect_stdout(io.StringIO()):
+        for fo in (True, False):
+            _, tau, G = R.tl_three_op_two_time(biexciton, t_axis, p, t_mem=0.5, opA="|3><1|_4", opB="|1><1|_4",
+                                               opC="|1><3|_4", tau_max=4.0, dt=0.1, rho0=rho0, options=opts(),
+                                               use_dm=True, fortran_only=fo)
+            out[f"g2_f{int(fo)}"] = G
+        _, tau, G = R.tl_two_op_two_time(biexciton, t_axis, p, t_mem=0.5, opA="|1><0|_4", opB="|0><1|_4",
+                                         tau_max=4.0, dt=0.1, rho0=rho0, options=opts(), use_dm=True,
+                                         fortran_only=False)
+        out["g1_f0"] = G
+    out["tau"] = tau
+    np.savez_compressed(os.path.join(HERE, "pyref_twotime_anchor.npz"), **out)
+
+
 def gen_purity():
     """two_time/purity.py bookkeeping and time-local-map paths: the REFERENCE Purity / Indistinguishability classes
     driven by tests/fake_system.fake_system_dm (analytic outputs + synthetic dynamical maps), with the reference
@@ -396,6 +512,8 @@ if __name__ == "__main__":
         raise SystemExit("build oracle/_ref first: make -C oracle ref")
     gen_fortran()
     gen_pyref()
+    gen_correlations()
+    gen_twotime_anchor()
     gen_polent()
     gen_purity()
     gen_g1()
