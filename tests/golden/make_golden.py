@@ -365,6 +365,56 @@ def gen_twotime_anchor():
     np.savez_compressed(os.path.join(HERE, "pyref_twotime_anchor.npz"), **out)
 
 
+def gen_params():
+    """the ACE param text (and %.8f pulse files) the REFERENCE model functions write, captured with
+    prepare_only=True (general_system.py:292-296; its module imports with the empty ACEutils placeholder of
+    _ref_correlations). Temp-file paths are replaced by tokens. tests/test_params_golden.py lowers the same calls
+    through our driver and checks every line's semantics (H0, Lindblad terms, pulse couplings and samples, initial
+    state, outputs, multi-time operators)."""
+    import io
+    import json
+    import contextlib
+    import tempfile
+    import warnings
+    warnings.simplefilter("ignore")
+    _ref_correlations()
+    from pyaceqd.pulses import ChirpedPulse  # noqa: E402
+    from pyaceqd.two_level_system.tls import tls  # noqa: E402
+    from pyaceqd.four_level_system.linear import biexciton  # noqa: E402
+    from pyaceqd.six_level_system.linear import sixls_linear  # noqa: E402
+    p1 = ChirpedPulse(tau_0=1.0, e_start=0.2, e0=1.3, t0=2.0, alpha=5.0, phase=0.3)
+    p2 = ChirpedPulse(tau_0=0.8, e_start=-1.0, e0=0.7, t0=3.0, polar_x=0.6)
+    mto = [{"operator": "|0><1|_2", "applyFrom": "_left", "applyBefore": "false", "time": 1.5},
+           {"operator": "|1><0|_2", "applyFrom": "_right", "time": 1.5},
+           {"operator": "|1><1|_2", "applyFrom": "", "applyBefore": "true", "time": 2.0}]
+    cases = {
+        "tls": (tls, dict(dt=0.1, lindblad=True, multitime_op=mto, gamma_e=0.02)),
+        "tls_dephasing": (tls, dict(dt=0.05, lindblad=True, dephasing=0.01, e_x=0.3)),
+        "biexciton": (biexciton, dict(dt=0.1, lindblad=True, delta_xy=0.1, delta_b=3.0, gamma_b=0.03)),
+        "sixls": (sixls_linear, dict(dt=0.1, bx=1.5, bz=0.5, lindblad=True)),
+    }
+    out = {}
+    for name, (fn, kw) in cases.items():
+        tmp = tempfile.mkdtemp() + "/"
+        with contextlib.redirect_stdout(io.StringIO()):
+            fn(0, 4, p1, p2, temp_dir=tmp, prepare_only=True, suffix="g", **kw)
+        files = sorted(os.listdir(tmp))
+        params = [f for f in files if f.endswith(".param")]
+        assert len(params) == 1, files
+        text = open(tmp + params[0]).read()
+        rec = {"kwargs": {k: v for k, v in kw.items()}, "pulse_files": {}}
+        for f in files:
+            if f.endswith(".dat"):
+                tok = "<PULSE_Y>" if "_y_" in f else "<PULSE_X>"
+                text = text.replace(tmp + f, tok)
+                rec["pulse_files"][tok] = open(tmp + f).read()
+        text = text.replace(tmp, "<TMP>/")
+        rec["param"] = text
+        out[name] = rec
+    with open(os.path.join(HERE, "pyref_params.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 def gen_purity():
     """two_time/purity.py bookkeeping and time-local-map paths: the REFERENCE Purity / Indistinguishability classes
     driven by tests/fake_system.fake_system_dm (analytic outputs + synthetic dynamical maps), with the reference
