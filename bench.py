@@ -246,11 +246,12 @@ def main():
             sp.execute()
         sp.synchronize()
         _, s_ms, _ = sp.timing(reset=True)
+        sp.download()  # raises on a split timeout that could not be recovered, or on non-finite outputs
+        path, bt, fallbacks = sp.info()
         line["single_run"] = {"workload": f"one biexciton G2 trajectory, chi={args.chi}, {args.n_tau} steps",
                               "sweep_ms": s_ms, "us_per_step": s_ms * 1e3 / (args.n_tau + 1),
                               "traj_steps_per_s": (args.n_tau + 1) / (s_ms * 1e-3),
-                              "path": "split groups (PQD_SPLIT)" if os.environ.get("PQD_SPLIT", "1") != "0"
-                              else "batched kernel"}
+                              "path": path, "split_fallbacks": fallbacks}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.chi, args.cpu_seconds)
     if rank == 0:

@@ -137,11 +137,22 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
                           pqd_plan** out);
 /* enqueue free-propagator build (if rebuild_free) + sweep on the context stream (asynchronous) */
 int pqd_plan_execute(pqd_plan* plan, int32_t rebuild_free);
-/* device pointer of the plan's output buffer (out_len complex values) */
+/* device pointer of the plan's output buffer (out_len complex values); valid after pqd_plan_synchronize */
 void* pqd_plan_output_device(pqd_plan* plan);
+/* wait for the last execute and check it: a split-group launch (PQD_PATH_SPLIT) that timed out because its
+ * workgroups could not all be resident (device shared with other work) is re-run on the batched kernel, and
+ * the plan stays batched; a NaN/Inf output returns PQD_ERR_NUMERIC. Replaces the reference's
+ * CalledProcessError on a failed ACE run (general_system.py:339-341). */
+int pqd_plan_synchronize(pqd_plan* plan);
+/* pqd_plan_synchronize + copy of the outputs (also on PQD_ERR_NUMERIC, which is still returned) */
 int pqd_plan_download(pqd_plan* plan, pqd_c128* out, int64_t out_len);
-/* average kernel durations (ms) of the executions since the last reset, from HIP events on the
- * launch stream: [0] free-propagator kernel, [1] sweep kernel; n = number of executions */
+#define PQD_PATH_NOPT 0     /* no PT: one wave per trajectory */
+#define PQD_PATH_BATCHED 1  /* lock-step PT sweep, bt trajectories per workgroup */
+#define PQD_PATH_SPLIT 2    /* one trajectory over N^2 workgroups (latency path) */
+/* the path the plan runs now, its trajectories per workgroup, and how many split launches fell back */
+int pqd_plan_info(const pqd_plan* plan, int32_t* path, int32_t* bt, int32_t* split_fallbacks);
+/* average kernel durations (ms) of the executions since the last reset (the most recent 64 at most),
+ * from HIP events on the launch stream: [0] free-propagator kernel, [1] sweep kernel; n = executions */
 int pqd_plan_timing(pqd_plan* plan, double* ms_free, double* ms_sweep, int32_t* n, int32_t reset);
 void pqd_plan_destroy(pqd_plan* plan);
 

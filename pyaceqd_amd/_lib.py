@@ -17,6 +17,10 @@ class PQDError(RuntimeError):
     pass
 
 
+class NumericError(PQDError):
+    """PQD_ERR_NUMERIC: a propagated output value is NaN or Inf"""
+
+
 class c128(C.Structure):
     _fields_ = [("re", C.c_double), ("im", C.c_double)]
 
@@ -72,7 +76,9 @@ _SIGS = {
                          C.c_int32, P_C128, C.POINTER(pqd_traj), C.c_int64, C.POINTER(C.c_void_p)], C.c_int),
     "pqd_plan_execute": ([C.c_void_p, C.c_int32], C.c_int),
     "pqd_plan_output_device": ([C.c_void_p], C.c_void_p),
+    "pqd_plan_synchronize": ([C.c_void_p], C.c_int),
     "pqd_plan_download": ([C.c_void_p, P_C128, C.c_int64], C.c_int),
+    "pqd_plan_info": ([C.c_void_p, P_I32, P_I32, P_I32], C.c_int),
     "pqd_plan_timing": ([C.c_void_p, P_F64, P_F64, P_I32, C.c_int32], C.c_int),
     "pqd_plan_destroy": ([C.c_void_p], None),
     "pqd_propagate_tau": ([C.c_void_p, P_C128, C.c_int32, P_C128, C.c_int32, C.c_int32, C.c_int32, P_C128], C.c_int),
@@ -116,7 +122,7 @@ def lib():
 def check(rc):
     if rc != 0:
         msg = lib().pqd_last_error().decode(errors="replace")
-        exc = ValueError if rc == 1 else PQDError
+        exc = ValueError if rc == 1 else NumericError if rc == 5 else PQDError
         raise exc(f"libpqd error {rc}: {msg}")
 
 

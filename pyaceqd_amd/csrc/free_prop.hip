@@ -325,8 +325,7 @@ hipError_t launch_fuse_steps(int N2, const FuseParams& p, hipStream_t s) {
 }
 
 hipError_t launch_free_prop(int N2, const FreePropParams& p, hipStream_t s) {
-    static const bool small4 = [] { const char* e = getenv("PQD_FP4"); return !e || atoi(e) != 0; }();
-    if (N2 == 4 && small4) {  // PQD_FP4=0: the general one-workgroup-per-matrix kernel (A/B)
+    if (N2 == 4 && p.packed4) {  // packed4 = 0 (PQD_FP4=0 at plan creation): the general kernel (A/B)
         const long long n_mat = (long long)p.n_sys * 2 * p.n_steps;
         if (n_mat <= 0) return hipSuccess;
         hipLaunchKernelGGL(free_prop4_kernel, dim3((unsigned)std::min<long long>((n_mat + 15) / 16, FP_MAX_BLOCKS)),

@@ -45,6 +45,7 @@ struct FreePropParams {
     double ta, dt;
     int n_steps, n_sub;
     double2* M;              // out: n_sys*2*n_steps*N2*N2
+    int packed4;             // N2 = 4: 16 matrices per workgroup (free_prop4_kernel); 0: the general kernel (A/B)
 };
 
 struct SweepParams {
@@ -83,7 +84,17 @@ struct SweepParams {
     int umax;                //   a unit with slice < 0 ends a wave's list; NULL: rows a = wave + k BT
     int trpre;               // 1: traces one lane per (trajectory, output, row), W rows fetched a step ahead
     int ablate;              // diagnostics only (PQD_ABLATE): 1 skip PT, 2 skip column phases, 4 skip outputs
+    int split_b128;          // split groups: 16-B sc1 exchange accesses (A/B switch, PQD_SPLIT_B128 at plan creation)
+    unsigned* flags;         // bit 0: a non-finite output was written (-> PQD_ERR_NUMERIC at synchronize/download)
+    unsigned spin_limit;     // split groups: polls before a wait for the peers times out (PQD_SPLIT_SPIN, tests)
 };
+
+// every output element goes through here: a NaN/Inf raises the plan's numeric flag (one vector atomic, taken only
+// on the failure path)
+__device__ __forceinline__ void out_store(double2* o, double2 v, unsigned* flags) {
+    *o = v;
+    if (!(__builtin_isfinite(v.x) && __builtin_isfinite(v.y))) atomicOr(flags, 1u);
+}
 
 // map-chain (Fortran f2py equivalents)
 struct MapChainParams {
@@ -149,6 +160,7 @@ hipError_t launch_dynamics_t1(const FourTimeParams& p, double2* out, hipStream_t
 hipError_t launch_tl_dynmap(const double2* dm, int n_maps, int n, double rcond, double2* out, hipStream_t s);
 int tl_dynmap_nmax();
 bool split_supported(int N2, int CHI, int n_traj, int n_cu);
+int split_blocks_per_cu(int N2, int CHI);
 hipError_t launch_split(int N2, int CHI, int n_traj, const SweepParams& p, double2* X, unsigned* cnt,
                         unsigned* err, hipStream_t s);
 bool sweep_supported(int N2, int CHI);

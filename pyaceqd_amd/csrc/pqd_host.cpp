@@ -216,8 +216,18 @@ struct pqd_plan {
     FreePropParams fp{};
     SweepParams sp{};
     int64_t out_len = 0;
-    std::vector<hipEvent_t> evs;  // triplets per execute
+    DevBuf<unsigned> flags;       // bit 0: non-finite output (PQD_ERR_NUMERIC)
+    int split_fallbacks = 0;      // split launches that timed out and were re-run on the batched kernel
+    // hipEvent triplets (start, free propagators done, sweep done) of the last RING executes, created once
+    static constexpr int RING = 64;
+    hipEvent_t ring[3 * RING] = {};
+    bool ring_ready = false;
+    int ev_head = 0, ev_count = 0;  // next slot; executes recorded since the last timing reset (<= RING kept)
     int32_t execs = 0;
+    ~pqd_plan() {
+        if (ring_ready)
+            for (auto& e : ring) (void)hipEventDestroy(e);
+    }
 };
 
 
@@ -360,6 +370,7 @@ int pqd_free_propagators(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* gr
     FreePropParams fp{};
     fp.systems = tab.p; fp.n_sys = 1;
     fp.ta = grid->ta; fp.dt = grid->dt; fp.n_steps = grid->n_steps; fp.n_sub = grid->n_sub; fp.M = M.p;
+    { const char* f4 = getenv("PQD_FP4"); fp.packed4 = (f4 && atoi(f4) == 0) ? 0 : 1; }
     HIPCHK(launch_free_prop(N2, fp, s));
     if (nM) HIPCHK(hipMemcpyAsync(M_out, M.p, nM * sizeof(double2), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -537,7 +548,11 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     {
         const char* e = getenv("PQD_SPLIT");
         const int mode = e ? atoi(e) : 1;
-        P->split = pt && mode != 0 && split_supported(N2, P->CHI, tr->n_traj, n_cu) && (mode == 2 || N2 >= 9);
+        // the spin hand-off needs every workgroup of a group resident: the occupancy the runtime reports for the
+        // split kernel (one workgroup per CU by its LDS request) must cover all n_traj * N2 workgroups
+        const int bpc = (pt && mode != 0) ? split_blocks_per_cu(N2, P->CHI) : 0;
+        P->split = pt && mode != 0 && bpc >= 1 && split_supported(N2, P->CHI, tr->n_traj, n_cu * bpc) &&
+                   (mode == 2 || N2 >= 9);
     }
     int BT = (sweep_max_bt(N2) >= 8 && tr->n_traj >= 8 * n_cu) ? 8 : 4;
     if (const char* e = getenv("PQD_BT")) BT = std::min(atoi(e) >= 8 ? 8 : 4, sweep_max_bt(N2));
@@ -581,6 +596,14 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     sp.blk_traj = P->blk_traj.p; sp.blk_end = P->blk_end.p; sp.blk_sys = P->blk_sys.p;
     sp.traj_sys = P->traj_sys.p; sp.m_stride = (long long)2 * ns * m2; sp.wbeg = P->wbeg.p; sp.wend = P->wend.p;
     { const char* ab = getenv("PQD_ABLATE"); sp.ablate = ab ? atoi(ab) : 0; }
+    { const char* b1 = getenv("PQD_SPLIT_B128"); sp.split_b128 = (b1 && atoi(b1) != 0) ? 1 : 0; }
+    // polls of a split group's counter before the wait counts as a timeout (~0.1 s); PQD_SPLIT_SPIN overrides
+    // it (tests provoke the batched fallback with 0)
+    { const char* sl = getenv("PQD_SPLIT_SPIN"); sp.spin_limit = sl ? (unsigned)strtoul(sl, nullptr, 10) : (1u << 22); }
+    { const char* f4 = getenv("PQD_FP4"); P->fp.packed4 = (f4 && atoi(f4) == 0) ? 0 : 1; }
+    HIPCHK(P->flags.alloc(4));
+    HIPCHK(hipMemsetAsync(P->flags.p, 0, 4 * sizeof(unsigned), s));
+    sp.flags = P->flags.p;
     { const char* pm = getenv("PQD_PT_MODE"); sp.pt_mode = pm ? atoi(pm) : 4; }
     { const char* c3 = getenv("PQD_CMUL3"); sp.cmul3 = c3 ? atoi(c3) : 1; }
     { const char* tp = getenv("PQD_TRPRE"); sp.trpre = tp ? atoi(tp) : 1; }
@@ -624,14 +647,18 @@ int pqd_plan_execute(pqd_plan* P, int32_t rebuild_free) {
     if (!P) return fail(PQD_ERR_ARG, "plan is NULL");
     HIPCHK(hipSetDevice(P->ctx->device));
     hipStream_t s = P->ctx->stream;
-    hipEvent_t e[3];
-    for (int i = 0; i < 3; ++i) HIPCHK(hipEventCreate(&e[i]));
+    if (!P->ring_ready) {
+        for (auto& e : P->ring) HIPCHK(hipEventCreate(&e));
+        P->ring_ready = true;
+    }
+    hipEvent_t* e = P->ring + 3 * P->ev_head;
     HIPCHK(hipEventRecord(e[0], s));
     if (rebuild_free && P->n_steps > 0) {
         HIPCHK(launch_free_prop(P->N2, P->fp, s));
         if (P->sp.fuse) HIPCHK(launch_fuse_steps(P->N2, P->fu, s));
     }
     HIPCHK(hipEventRecord(e[1], s));
+    HIPCHK(hipMemsetAsync(P->flags.p, 0, sizeof(unsigned), s));
     if (P->nopt)
         HIPCHK(launch_sweep_nopt(P->N2, P->n_traj, P->sp, s));
     else if (P->split)
@@ -639,23 +666,58 @@ int pqd_plan_execute(pqd_plan* P, int32_t rebuild_free) {
     else
         HIPCHK(launch_sweep(P->N2, P->CHI, P->BT, P->n_blocks, P->sp, s));
     HIPCHK(hipEventRecord(e[2], s));
-    for (int i = 0; i < 3; ++i) P->evs.push_back(e[i]);
+    P->ev_head = (P->ev_head + 1) % pqd_plan::RING;
+    P->ev_count++;
     P->execs++;
     return PQD_OK;
 }
 
 void* pqd_plan_output_device(pqd_plan* P) { return P ? (void*)P->out.p : nullptr; }
 
+// Wait for the plan's last execute and check it. A split launch whose groups could not all be resident (the device
+// is shared with other work, so a peer workgroup never arrived) ends with its error word set: the plan then re-runs
+// the same step range on the batched kernel, which needs no co-residency, and stays on it. A non-finite output
+// value raises PQD_ERR_NUMERIC.
+int pqd_plan_synchronize(pqd_plan* P) {
+    if (!P) return fail(PQD_ERR_ARG, "plan is NULL");
+    HIPCHK(hipSetDevice(P->ctx->device));
+    hipStream_t s = P->ctx->stream;
+    if (P->split) {
+        unsigned err = 0;
+        HIPCHK(hipMemcpyAsync(&err, P->err.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (err) {
+            P->split = false;
+            P->split_fallbacks++;
+            HIPCHK(hipMemsetAsync(P->err.p, 0, sizeof(unsigned), s));
+            HIPCHK(hipMemsetAsync(P->flags.p, 0, sizeof(unsigned), s));
+            HIPCHK(launch_sweep(P->N2, P->CHI, P->BT, P->n_blocks, P->sp, s));
+        }
+    }
+    unsigned flags = 0;
+    HIPCHK(hipMemcpyAsync(&flags, P->flags.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (flags & 1u) return fail(PQD_ERR_NUMERIC, "non-finite value (NaN/Inf) in the propagated outputs");
+    return PQD_OK;
+}
+
 int pqd_plan_download(pqd_plan* P, pqd_c128* out, int64_t out_len) {
     if (!P || !out) return fail(PQD_ERR_ARG, "NULL argument");
     if (out_len < P->out_len) return fail(PQD_ERR_ARG, "out_len %lld < plan out_len %lld", (long long)out_len, (long long)P->out_len);
-    HIPCHK(hipSetDevice(P->ctx->device));
-    if (P->out_len > 0)
+    int rc = pqd_plan_synchronize(P);
+    if (rc && rc != PQD_ERR_NUMERIC) return rc;
+    if (P->out_len > 0) {
         HIPCHK(hipMemcpyAsync(out, P->out.p, P->out_len * sizeof(double2), hipMemcpyDeviceToHost, P->ctx->stream));
-    unsigned err = 0;
-    if (P->split) HIPCHK(hipMemcpyAsync(&err, P->err.p, sizeof(unsigned), hipMemcpyDeviceToHost, P->ctx->stream));
-    HIPCHK(hipStreamSynchronize(P->ctx->stream));
-    if (err) return fail(PQD_ERR_HIP, "split sweep: a workgroup group timed out waiting for its peers");
+        HIPCHK(hipStreamSynchronize(P->ctx->stream));
+    }
+    return rc;  // PQD_ERR_NUMERIC still hands the values over (they show where the run went bad)
+}
+
+int pqd_plan_info(const pqd_plan* P, int32_t* path, int32_t* bt, int32_t* split_fallbacks) {
+    if (!P) return fail(PQD_ERR_ARG, "plan is NULL");
+    if (path) *path = P->nopt ? PQD_PATH_NOPT : P->split ? PQD_PATH_SPLIT : PQD_PATH_BATCHED;
+    if (bt) *bt = P->BT;
+    if (split_fallbacks) *split_fallbacks = P->split_fallbacks;
     return PQD_OK;
 }
 
@@ -663,21 +725,20 @@ int pqd_plan_timing(pqd_plan* P, double* ms_free, double* ms_sweep, int32_t* n, 
     if (!P) return fail(PQD_ERR_ARG, "plan is NULL");
     HIPCHK(hipSetDevice(P->ctx->device));
     double f = 0, w = 0;
-    const int k = (int)P->evs.size() / 3;
+    const int k = std::min(P->ev_count, pqd_plan::RING);  // the most recent k executes
     for (int i = 0; i < k; ++i) {
+        const int slot = ((P->ev_head - 1 - i) % pqd_plan::RING + pqd_plan::RING) % pqd_plan::RING;
+        hipEvent_t* e = P->ring + 3 * slot;
         float a = 0, b = 0;
-        HIPCHK(hipEventSynchronize(P->evs[3 * i + 2]));
-        HIPCHK(hipEventElapsedTime(&a, P->evs[3 * i], P->evs[3 * i + 1]));
-        HIPCHK(hipEventElapsedTime(&b, P->evs[3 * i + 1], P->evs[3 * i + 2]));
+        HIPCHK(hipEventSynchronize(e[2]));
+        HIPCHK(hipEventElapsedTime(&a, e[0], e[1]));
+        HIPCHK(hipEventElapsedTime(&b, e[1], e[2]));
         f += a; w += b;
     }
     if (ms_free) *ms_free = k ? f / k : 0.0;
     if (ms_sweep) *ms_sweep = k ? w / k : 0.0;
     if (n) *n = k;
-    if (reset) {
-        for (auto ev : P->evs) (void)hipEventDestroy(ev);
-        P->evs.clear();
-    }
+    if (reset) P->ev_count = 0;
     return PQD_OK;
 }
 
@@ -685,7 +746,6 @@ void pqd_plan_destroy(pqd_plan* P) {
     if (!P) return;
     (void)hipSetDevice(P->ctx->device);
     (void)hipStreamSynchronize(P->ctx->stream);
-    for (auto ev : P->evs) (void)hipEventDestroy(ev);
     delete P;
 }
 

@@ -30,7 +30,6 @@ typedef unsigned int __attribute__((address_space(1))) gu32;
 
 constexpr int SP_NT = 256;
 constexpr int SP_LDS_FORCE = 96 * 1024;  // dynamic LDS request: one workgroup per CU
-constexpr unsigned SP_SPIN_LIMIT = 1u << 22;
 
 __device__ __forceinline__ void st_sc1(double2* p, double2 v) {
     __hip_atomic_store((gu64*)&p->x, (unsigned long long)__double_as_longlong(v.x), __ATOMIC_RELAXED,
@@ -156,7 +155,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
             double2 s = c_zero();
 #pragma unroll
             for (int b = 0; b < N2; ++b) c_fma(s, gld(w + (size_t)k * N2 + b), smem[RRO + b]);
-            p.out[wo + (long long)(n - wb) * p.n_out + k] = s;
+            out_store(p.out + wo + (long long)(n - wb) * p.n_out + k, s, p.flags);
         }
     };
     auto has_event = [&](int n) { return ev_cur < ev_lim && p.ev[ev_cur].x == n; };
@@ -234,7 +233,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
             bool ok = true;
             while (__hip_atomic_load((gu32*)ct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
                 __builtin_amdgcn_s_sleep(1);
-                if (++spins > SP_SPIN_LIMIT) { ok = false; break; }
+                if (++spins > p.spin_limit) { ok = false; break; }
             }
             if (tid == 0) {
                 s_abort = ok ? 0 : 1;
@@ -270,9 +269,9 @@ hipError_t launch_split_tb(int n_traj, const SweepParams& p, double2* X, unsigne
 
 template <int N2, int CHI>
 hipError_t launch_split_t(int n_traj, const SweepParams& p, double2* X, unsigned* cnt, unsigned* err, hipStream_t s) {
-    // PQD_SPLIT_B128=1: 16-B sc1 buffer accesses for the exchange (A/B switch; 0 = two 8-B atomics per element)
-    static const bool b128 = [] { const char* e = getenv("PQD_SPLIT_B128"); return e && atoi(e) != 0; }();
-    return b128 ? launch_split_tb<N2, CHI, true>(n_traj, p, X, cnt, err, s)
+    // p.split_b128 (PQD_SPLIT_B128=1 at plan creation): 16-B sc1 buffer accesses for the exchange (A/B switch;
+    // 0 = two 8-B atomics per element)
+    return p.split_b128 ? launch_split_tb<N2, CHI, true>(n_traj, p, X, cnt, err, s)
                 : launch_split_tb<N2, CHI, false>(n_traj, p, X, cnt, err, s);
 }
 
@@ -287,7 +286,41 @@ hipError_t launch_split_n(int CHI, int n_traj, const SweepParams& p, double2* X,
     }
 }
 
+template <int N2, int CHI>
+int split_occ_t() {
+    using L = SplitLayout<N2, CHI>;
+    if (hipFuncSetAttribute((const void*)pt_split_kernel<N2, CHI, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)L::LDS) != hipSuccess)
+        return 0;
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, pt_split_kernel<N2, CHI, false>, SP_NT, L::LDS) != hipSuccess)
+        return 0;
+    return nb;
+}
+
+template <int N2>
+int split_occ_n(int CHI) {
+    switch (CHI) {
+        case 16: return split_occ_t<N2, 16>();
+        case 32: return split_occ_t<N2, 32>();
+        case 64: return split_occ_t<N2, 64>();
+        default: return 0;
+    }
+}
+
 }  // namespace
+
+// workgroups of the split kernel the runtime can keep resident per CU (0: the kernel cannot run)
+int split_blocks_per_cu(int N2, int CHI) {
+    switch (N2) {
+        case 4: return split_occ_n<4>(CHI);
+        case 9: return split_occ_n<9>(CHI);
+        case 16: return split_occ_n<16>(CHI);
+        case 25: return split_occ_n<25>(CHI);
+        case 36: return split_occ_n<36>(CHI);
+        default: return 0;
+    }
+}
 
 bool split_supported(int N2, int CHI, int n_traj, int n_cu) {
     return (CHI == 16 || CHI == 32 || CHI == 64) &&

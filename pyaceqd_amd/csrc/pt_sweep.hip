@@ -451,7 +451,8 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(BT, CHI)) void pt_sweep_kernel(
                     double2 x = c_mul(v, rbuf[b * N2 + a]);
 #pragma unroll
                     for (int m = 1; m < N2; m <<= 1) x = c_add(x, c_shfl_xor(x, m));
-                    if (a == 0 && s_wb[b] <= n && n <= s_we[b]) outg[s_wo[b] + (long long)(n - s_wb[b]) * p.n_out + k] = x;
+                    if (a == 0 && s_wb[b] <= n && n <= s_we[b])
+                        out_store(outg + s_wo[b] + (long long)(n - s_wb[b]) * p.n_out + k, x, p.flags);
                 }
             } else
             for (int e = tid; e < BT * p.n_out; e += NT) {
@@ -474,7 +475,7 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(BT, CHI)) void pt_sweep_kernel(
                         for (int j = 0; j < CK; ++j)
                             if (a0 + j < N2) c_fma(s, ovr[j], rbuf[b * N2 + a0 + j]);
                     }
-                    outg[s_wo[b] + (long long)(n - s_wb[b]) * p.n_out + k] = s;
+                    out_store(outg + s_wo[b] + (long long)(n - s_wb[b]) * p.n_out + k, s, p.flags);
                 }
             }
         }
@@ -662,17 +663,20 @@ __global__ __launch_bounds__(64) void sweep_nopt_kernel(SweepParams p) {
         own = lane_apply<N2>(p.sop + (size_t)e.z * N2 * N2, own, lane);
         ++ev_cur;
     }
-    const int k = lane < p.n_out ? lane : p.n_out - 1;
     for (int n = 0;; ++n) {
         if (wb <= n && n <= we) {
-            double2 s = c_zero();
-            const double2* ov = p.ovec + (size_t)k * N2;
+            // every lane gathers the state (all lanes take part in the shuffles), then lane k owns outputs
+            // k, k + 64, ... (n_out may exceed the wave)
+            double2 x[N2];
 #pragma unroll
-            for (int a = 0; a < N2; ++a) {
-                const double2 x = make_double2(__shfl(own.x, a), __shfl(own.y, a));
-                c_fma(s, ov[a], x);
+            for (int a = 0; a < N2; ++a) x[a] = make_double2(__shfl(own.x, a), __shfl(own.y, a));
+            for (int k = lane; k < p.n_out; k += 64) {
+                double2 s = c_zero();
+                const double2* ov = p.ovec + (size_t)k * N2;
+#pragma unroll
+                for (int a = 0; a < N2; ++a) c_fma(s, ov[a], x[a]);
+                out_store(p.out + wo + (long long)(n - wb) * p.n_out + k, s, p.flags);
             }
-            if (lane < p.n_out) p.out[wo + (long long)(n - wb) * p.n_out + lane] = s;
         }
         if (n >= we) break;
         while (ev_cur < ev_lim) {

@@ -289,7 +289,17 @@ class Plan:
         _lib.check(_lib.lib().pqd_plan_execute(self.handle, 1 if rebuild_free else 0))
 
     def synchronize(self):
-        self.ctx.synchronize()
+        """wait for the last execute; re-runs a timed-out split launch on the batched kernel, raises
+        _lib.NumericError on NaN/Inf outputs"""
+        _lib.check(_lib.lib().pqd_plan_synchronize(self.handle))
+
+    PATHS = {0: "no PT (one wave per trajectory)", 1: "batched lock-step sweep", 2: "split groups"}
+
+    def info(self):
+        """(path name, trajectories per workgroup, split launches that fell back to the batched kernel)"""
+        p, b, f = C.c_int32(), C.c_int32(), C.c_int32()
+        _lib.check(_lib.lib().pqd_plan_info(self.handle, C.byref(p), C.byref(b), C.byref(f)))
+        return self.PATHS[p.value], b.value, f.value
 
     def output_device_ptr(self):
         return _lib.lib().pqd_plan_output_device(self.handle)
