@@ -102,11 +102,49 @@ def pmc_traffic(cfg):
     return float(rec["hbm_bytes_per_launch"]), "profiles/pmc_traffic.json (" + rec.get("passes", "") + ")"
 
 
+def host_cpu():
+    """what the CPU baseline runs on: model, logical CPUs of the machine, CPUs this process may use (affinity and
+    cgroup quota), and whether the reference's ACE binary exists here"""
+    import shutil
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    aff = len(os.sched_getaffinity(0))
+    return {"model": model, "nproc": os.cpu_count(), "affinity": aff, "cgroup_cpus": quota,
+            "ace_binary": shutil.which("ACE")}
+
+
+def cpu_threads(info):
+    """threads for the CPU baseline: every CPU this process may use. The affinity mask and the cgroup quota bound
+    it; when neither does (a GPU box shows the whole multi-GPU machine), the box's documented CPU share per GPU
+    (16, the OMP_NUM_THREADS the box exports) is used instead of oversubscribing other tenants' cores."""
+    n = info["affinity"]
+    if info["cgroup_cpus"]:
+        n = min(n, max(1, int(info["cgroup_cpus"])))
+    elif n > 64:
+        n = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    return max(1, n)
+
+
 def cpu_baseline(chi, target_s=15.0):
     """oracle/liboracle.so (plain-C port, OpenMP over trajectories) on a bounded sample of the same workload"""
     from oracle import oracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
-    threads = max(1, min(threads, 16))
+    info = host_cpu()
+    threads = cpu_threads(info)
     # calibrate on the same shape with all threads (setup + free propagators included, as in the sample)
     n_traj = 2 * threads
     sysd, grid, pt, rho0, ops, tr = build_workload(n_traj, 300, chi)
@@ -121,7 +159,7 @@ def cpu_baseline(chi, target_s=15.0):
     oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt, nthreads=threads)
     el = time.perf_counter() - t0
     executed = int(np.sum(tr.out_end + 1))
-    return {"value": executed / el, "unit": "traj-steps/s", "cores": threads, "kind": "port",
+    return {"value": executed / el, "unit": "traj-steps/s", "cores": threads, "kind": "port", "host": info,
             "sample": f"{n_traj} trajectories x {steps} tau-steps (executed {executed} traj-steps incl. trunk and "
                       f"free-propagator build), chi={chi}, N=4, {el:.1f} s, oracle/pqd_oracle.c OpenMP"}
 
@@ -196,7 +234,7 @@ def main():
     assert np.all(np.isfinite(g0)), "non-finite output"
 
     useful = n_traj * args.n_tau
-    executed = int(np.sum(tr.out_end + 1))
+    executed = plan.traj_steps()   # shared trunks (PQD_BRANCH) counted once per workgroup
     value = useful * args.steps * world / el
     fused = os.environ.get("PQD_FUSE", "1") != "0"
     F = flops_per_traj_step(4, args.chi, len(ops), fused=fused)

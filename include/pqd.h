@@ -149,8 +149,10 @@ int pqd_plan_download(pqd_plan* plan, pqd_c128* out, int64_t out_len);
 #define PQD_PATH_NOPT 0     /* no PT: one wave per trajectory */
 #define PQD_PATH_BATCHED 1  /* lock-step PT sweep, bt trajectories per workgroup */
 #define PQD_PATH_SPLIT 2    /* one trajectory over N^2 workgroups (latency path) */
-/* the path the plan runs now, its trajectories per workgroup, and how many split launches fell back */
-int pqd_plan_info(const pqd_plan* plan, int32_t* path, int32_t* bt, int32_t* split_fallbacks);
+/* the path the plan runs now, its trajectories per workgroup, how many split launches fell back, and the
+ * trajectory-steps one execute propagates (trajectories of one system that share a lock-step workgroup propagate
+ * their common MTO-free trunk once: PQD_BRANCH) */
+int pqd_plan_info(const pqd_plan* plan, int32_t* path, int32_t* bt, int32_t* split_fallbacks, int64_t* traj_steps);
 /* average kernel durations (ms) of the executions since the last reset (the most recent 64 at most),
  * from HIP events on the launch stream: [0] free-propagator kernel, [1] sweep kernel; n = executions */
 int pqd_plan_timing(pqd_plan* plan, double* ms_free, double* ms_sweep, int32_t* n, int32_t reset);

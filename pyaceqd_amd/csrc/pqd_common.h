@@ -63,6 +63,13 @@ struct SweepParams {
     const int* blk_traj;     // n_blocks*BT trajectory ids (-1: empty slot)
     const int* blk_end;      // n_blocks: last step of the block (max out_end)
     const int* blk_sys;      // n_blocks: system of the block's first trajectory (waves index traj_sys)
+    const int* blk_act;      // n_blocks*BT: step at which the slot becomes active (shared trunk, see pqd_host.cpp
+                             //   branch_slots; 0 = from the start, INT_MAX = empty slot)
+    const int* blk_src;      // n_blocks*BT: at activation copy the (state, fused flag) of this slot (>= 0), or load
+                             //   checkpoint -2 - src of the trunk pre-pass (<= -2; fused flag 1); -1: fresh start
+    double2* ck;             // trunk checkpoints [n_ck][N2][CHI] (dense rows): augmented state at the top of a step
+    const int* ck_map;       // trunk pre-pass only: ck_map[t * ck_stride + n] = checkpoint written at the top of step
+    long long ck_stride;     //   n by trajectory t (-1: none); NULL in the main sweep
     const int* traj_sys;     // n_traj: system of each trajectory (chi = 1 kernel)
     long long m_stride;      // complex elements between the free propagators of consecutive systems
     const int* wbeg;         // per trajectory
@@ -85,16 +92,11 @@ struct SweepParams {
     int trpre;               // 1: traces one lane per (trajectory, output, row), W rows fetched a step ahead
     int ablate;              // diagnostics only (PQD_ABLATE): 1 skip PT, 2 skip column phases, 4 skip outputs
     int split_b128;          // split groups: 16-B sc1 exchange accesses (A/B switch, PQD_SPLIT_B128 at plan creation)
-    unsigned* flags;         // bit 0: a non-finite output was written (-> PQD_ERR_NUMERIC at synchronize/download)
+    unsigned* flags;         // bit 0: a non-finite output value (set by launch_check_finite at synchronize)
     unsigned spin_limit;     // split groups: polls before a wait for the peers times out (PQD_SPLIT_SPIN, tests)
 };
 
-// every output element goes through here: a NaN/Inf raises the plan's numeric flag (one vector atomic, taken only
-// on the failure path)
-__device__ __forceinline__ void out_store(double2* o, double2 v, unsigned* flags) {
-    *o = v;
-    if (!(__builtin_isfinite(v.x) && __builtin_isfinite(v.y))) atomicOr(flags, 1u);
-}
+
 
 // map-chain (Fortran f2py equivalents)
 struct MapChainParams {
@@ -138,10 +140,15 @@ struct FuseParams {          // F(m) = M_a(m) M_b(m-1) (1 <= m < n_steps), W(m) 
 };
 
 hipError_t launch_free_prop(int N2, const FreePropParams& p, hipStream_t s);
+// flags |= 1 if any of the n complex values is NaN or Inf (one pass over the output buffer at synchronize: the sweep
+// kernels carry no per-store check, which cost 1.7% of the headline kernel)
+hipError_t launch_check_finite(const double2* v, int64_t n, unsigned* flags, hipStream_t s);
 hipError_t launch_fuse_steps(int N2, const FuseParams& p, hipStream_t s);
 // waves per trajectory in the PT sweep: a 4-trajectory workgroup (N2 > 16 or chi = 128) runs 8 waves, two per
 // trajectory (each owns half of the bond columns in the column phases), so every SIMD holds two waves
-constexpr int sweep_wpt(int BT, int CHI) { return (BT == 4 && CHI >= 32) ? 2 : 1; }
+// (N2 = 4 included: one wave per trajectory there, four waves per workgroup and two workgroups per CU, measured
+// slower on the TLS scan, 38.4 -> 68.8 ms, profiles/r02/cfg_c2_bt4.log)
+constexpr int sweep_wpt(int N2, int BT, int CHI) { return (BT == 4 && CHI >= 32) ? 2 : 1; }
 // rows per PT unit (rows sharing one dictionary slice contracted together): 3 R (BT/4) (CHI/16) accumulators <= 48
 // (quads only at N2 > 16, where the 4-trajectory slice stream is L2-bound; smaller N2 keep pairs)
 constexpr int sweep_rmax(int N2, int BT, int CHI) {

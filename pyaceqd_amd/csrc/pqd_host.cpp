@@ -7,6 +7,7 @@
 #include "pqd_common.h"
 
 #include <algorithm>
+#include <climits>
 #include <memory>
 #include <complex>
 #include <cstdarg>
@@ -210,7 +211,20 @@ struct pqd_plan {
     DevBuf<double2> L0, S, T, samples, M, F, W, rho0, ovec, sop, out;
     DevBuf<FreePropSys> systab;
     FuseParams fu{};
-    DevBuf<int> sched, blk_traj, blk_end, blk_sys, traj_sys, wbeg, wend, ev_start;
+    DevBuf<int> sched, blk_traj, blk_end, blk_sys, blk_act, blk_src, traj_sys, wbeg, wend, ev_start;
+    int64_t traj_steps = 0;       // executed trajectory-steps per execute (shared trunks counted once)
+    int branch = 1;               // shared-trunk activation in the batched sweep (PQD_BRANCH)
+    // trunk pre-pass (pqd_host.cpp plan_trunks): one MTO-free trajectory per system writes the checkpoints the
+    // main sweep's slots start from
+    int n_trunk = 0, tk_blocks = 0, tk_BT = 4;
+    bool tk_split = false;
+    SweepParams tk{};
+    DevBuf<double2> ck, tk_out, tk_Xs;
+    DevBuf<int> tk_ckmap, tk_wbeg, tk_wend, tk_evstart, tk_tsys, tk_blk_traj, tk_blk_end, tk_blk_sys, tk_blk_act,
+        tk_blk_src;
+    DevBuf<long long> tk_woff;
+    DevBuf<int4> tk_units;
+    DevBuf<unsigned> tk_cnt, tk_err;
     DevBuf<long long> woff;
     DevBuf<int4> ev, units;
     FreePropParams fp{};
@@ -413,6 +427,128 @@ static std::vector<int4> pt_row_units(const std::vector<int>& gmap, int NW, int 
     return out;
 }
 
+// Shared trunks inside a lock-step block (the reference re-propagates 0 -> t1 in every trajectory of a two-time
+// sweep: correlations.py:155-169, pol_entanglement/G2.py:486-497). j[t] = the last step at whose top (before its
+// outputs) trajectory t still holds the MTO-free state: its first MTO's step if that MTO applies after the output,
+// one less if it applies before. Slots are ordered by j; slot k becomes active at
+// act[k] = min(j_k, out_begin_k, j_m) by copying the (state, fused flag) of an earlier slot m of the same system that
+// is already active then (act[m] < act[k]) and still MTO-free (j_m >= act[k]); before that it is dormant (no column
+// phases, its PT rows skipped where a whole row block is dormant). Outputs before act[k] are never needed
+// (act[k] <= out_begin_k), so every trajectory's outputs are those of its own full run.
+static void branch_slots(int BT, const int* members, const std::vector<int>& jv, const int32_t* out_begin,
+                         const std::vector<int>& tsys, bool enable, int* act, int* src) {
+    for (int k = 0; k < BT; ++k) {
+        const int t = members[k];
+        src[k] = -1;
+        if (t < 0) { act[k] = INT_MAX; continue; }
+        act[k] = 0;
+        if (!enable) continue;
+        const int a = std::min(jv[t], out_begin[t]);
+        int best = 0, bm = -1;
+        for (int m = 0; m < k; ++m) {
+            const int tm = members[m];
+            if (tm < 0 || tsys[tm] != tsys[t]) continue;
+            const int cand = std::min(a, jv[tm]);
+            if (act[m] < cand && cand > best) { best = cand; bm = m; }
+        }
+        if (bm >= 0) { act[k] = best; src[k] = bm; }
+    }
+}
+
+// Trunk pre-pass of a plan: one MTO-free trajectory per system that has checkpoints, propagated from step 0 to
+// its last checkpoint step, writing the augmented state at the top of every checkpoint step (ck_steps[y], indices
+// ck_base[y] + k). It runs before the main sweep on split groups when those fit (N2 >= 9, as in auto mode), else
+// as batched workgroups of four; the batched layout is always built (fallback after a split timeout).
+static int plan_trunks(pqd_plan* P, pqd_ctx* ctx, int n_sys, const std::vector<std::vector<int>>& ck_steps,
+                       const std::vector<int>& ck_base, int n_ck, int n_cu, int N2, int n_out, const pqd_pt* pt,
+                       hipStream_t s) {
+    const int ns = P->n_steps, CHI = P->CHI;
+    std::vector<int> wb, we, ts, map;
+    std::vector<long long> wo;
+    for (int y = 0; y < n_sys; ++y) {
+        if (ck_steps[y].empty()) continue;
+        const int t = (int)ts.size(), L = ck_steps[y].back();
+        ts.push_back(y);
+        wb.push_back(L);
+        we.push_back(L);
+        wo.push_back((long long)t * n_out);
+        map.resize((size_t)(t + 1) * (ns + 1), -1);
+        for (size_t k = 0; k < ck_steps[y].size(); ++k) map[(size_t)t * (ns + 1) + ck_steps[y][k]] = ck_base[y] + (int)k;
+        P->traj_steps += L + 1;
+    }
+    const int nt = (int)ts.size();
+    P->n_trunk = nt;
+    if (!nt) return PQD_OK;
+    std::vector<int> evs0(nt + 1, 0);
+    HIPCHK(P->ck.alloc((size_t)n_ck * N2 * CHI));
+    HIPCHK(P->tk_out.alloc((size_t)nt * n_out));
+    HIPCHK(P->tk_ckmap.upload(map.data(), map.size(), s));
+    HIPCHK(P->tk_wbeg.upload(wb.data(), nt, s));
+    HIPCHK(P->tk_wend.upload(we.data(), nt, s));
+    HIPCHK(P->tk_woff.upload(wo.data(), nt, s));
+    HIPCHK(P->tk_tsys.upload(ts.data(), nt, s));
+    HIPCHK(P->tk_evstart.upload(evs0.data(), evs0.size(), s));
+    // batched layout: four trunks per workgroup
+    const int BT = 4;
+    std::vector<int> bt, be, bs, ba, bsrc;
+    for (int t = 0; t < nt; t += BT) {
+        int end = 0;
+        for (int q = 0; q < BT; ++q) {
+            const int u = t + q < nt ? t + q : -1;
+            bt.push_back(u);
+            ba.push_back(u >= 0 ? 0 : INT_MAX);
+            bsrc.push_back(-1);
+            if (u >= 0) end = std::max(end, we[u]);
+        }
+        be.push_back(end);
+        bs.push_back(ts[t]);
+    }
+    P->tk_BT = BT;
+    P->tk_blocks = (int)be.size();
+    HIPCHK(P->tk_blk_traj.upload(bt.data(), bt.size(), s));
+    HIPCHK(P->tk_blk_end.upload(be.data(), be.size(), s));
+    HIPCHK(P->tk_blk_sys.upload(bs.data(), bs.size(), s));
+    HIPCHK(P->tk_blk_act.upload(ba.data(), ba.size(), s));
+    HIPCHK(P->tk_blk_src.upload(bsrc.data(), bsrc.size(), s));
+    {
+        const int nw = BT * sweep_wpt(N2, BT, CHI);
+        std::vector<int4> u = pt_row_units(pt->gmap_h, nw, sweep_rmax(N2, BT, CHI));
+        HIPCHK(P->tk_units.upload(u.data(), u.size(), s));
+    }
+    const int bpc = split_blocks_per_cu(N2, CHI);
+    const char* e = getenv("PQD_SPLIT");
+    const int mode = e ? atoi(e) : 1;
+    P->tk_split = mode != 0 && N2 >= 9 && bpc >= 1 && split_supported(N2, CHI, nt, n_cu * bpc);
+    HIPCHK(P->tk_Xs.alloc((size_t)nt * 2 * N2 * CHI));
+    HIPCHK(P->tk_cnt.alloc((size_t)nt * 32));
+    HIPCHK(P->tk_err.alloc(4));
+    (void)ctx;
+    return PQD_OK;
+}
+
+// the trunk pre-pass launch parameters: the main sweep's, with the trunk trajectories and checkpoint map
+static void finalize_trunks(pqd_plan* P) {
+    P->sp.ck = P->ck.p;
+    P->sp.ck_map = nullptr;
+    if (!P->n_trunk) return;
+    SweepParams& k = P->tk;
+    k = P->sp;
+    k.blk_traj = P->tk_blk_traj.p; k.blk_end = P->tk_blk_end.p; k.blk_sys = P->tk_blk_sys.p;
+    k.blk_act = P->tk_blk_act.p; k.blk_src = P->tk_blk_src.p;
+    k.traj_sys = P->tk_tsys.p; k.wbeg = P->tk_wbeg.p; k.wend = P->tk_wend.p; k.woff = P->tk_woff.p;
+    k.ev_start = P->tk_evstart.p; k.out = P->tk_out.p;
+    k.ck_map = P->tk_ckmap.p; k.ck_stride = P->n_steps + 1;
+    const int nw = P->tk_BT * sweep_wpt(P->N2, P->tk_BT, P->CHI);
+    k.units = (P->sp.units ? P->tk_units.p : nullptr);
+    k.umax = (int)(P->tk_units.n / nw);
+}
+
+static hipError_t launch_trunks(pqd_plan* P, hipStream_t s) {
+    if (!P->n_trunk) return hipSuccess;
+    if (P->tk_split) return launch_split(P->N2, P->CHI, P->n_trunk, P->tk, P->tk_Xs.p, P->tk_cnt.p, P->tk_err.p, s);
+    return launch_sweep(P->N2, P->CHI, P->tk_BT, P->tk_blocks, P->tk, s);
+}
+
 int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems, const int32_t* traj_sys,
                           const pqd_grid* grid, const pqd_pt* pt, const int32_t* sched, const pqd_c128* rho0,
                           int32_t n_out, const pqd_c128* out_ops, const pqd_traj* tr, int64_t out_len,
@@ -528,11 +664,19 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     HIPCHK(P->woff.upload(reinterpret_cast<const long long*>(tr->out_offset), std::max(1, tr->n_traj), s));
     std::vector<int> order(tr->n_traj);
     for (int t = 0; t < tr->n_traj; ++t) order[t] = t;
+    // j[t]: last step whose top still sees the MTO-free state (branch_slots)
+    std::vector<int> jv(std::max(1, tr->n_traj), 0);
+    for (int t = 0; t < tr->n_traj; ++t) {
+        if (ev_start[t] == ev_start[t + 1]) { jv[t] = tr->out_end[t]; continue; }
+        const int4 e = evs[ev_start[t]];
+        jv[t] = e.y == 1 ? e.x : e.x - 1;
+    }
     // group by system (a workgroup whose trajectories share one system reads one set of free propagators),
-    // longest first inside a system
+    // longest first inside a system, then by branch step (neighbouring slots share the longest trunk)
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
         if (tsys[a] != tsys[b]) return tsys[a] < tsys[b];
-        return tr->out_end[a] > tr->out_end[b];
+        if (tr->out_end[a] != tr->out_end[b]) return tr->out_end[a] > tr->out_end[b];
+        return jv[a] < jv[b];
     });
     // trajectories per workgroup: 8 (half the PT-slice L2 traffic per trajectory) when the LDS allows it
     // and the batch still fills every CU, else 4
@@ -558,27 +702,103 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     if (const char* e = getenv("PQD_BT")) BT = std::min(atoi(e) >= 8 ? 8 : 4, sweep_max_bt(N2));
     if (P->CHI > 64) BT = 4;  // chi = 128: only four augmented states fit the LDS
     P->BT = BT;
-    std::vector<int> bt, be, bs;
+    std::vector<int> bt, be, bs, ba, bsrc;
+    {
+        const char* e = getenv("PQD_BRANCH");
+        P->branch = (e && atoi(e) == 0) ? 0 : 1;
+    }
+    const bool fuse_on = !P->nopt && ns > 0 && [] { const char* f = getenv("PQD_FUSE"); return f ? atoi(f) != 0 : true; }();
+    const bool branch_on = P->branch != 0 && pt != nullptr && !P->split;
     // blocks are filled in this order and may straddle systems (each wave indexes its own system's propagators),
     // so a scan with one trajectory per system still fills every slot of a workgroup
     for (size_t k = 0; k < order.size();) {
         const int sy = tsys[order[k]];
         int filled = 0, end = 0;
+        const size_t b0 = bt.size();
         while (k < order.size() && filled < BT) {
             bt.push_back(order[k]);
             end = std::max(end, tr->out_end[order[k]]);
             ++k; ++filled;
         }
         for (; filled < BT; ++filled) bt.push_back(-1);
+        // slots by branch step (empty ones last): the trunk passes from slot to slot
+        std::stable_sort(bt.begin() + b0, bt.end(), [&](int a, int b) {
+            if (a < 0 || b < 0) return a >= 0 && b < 0;
+            return jv[a] < jv[b];
+        });
+        ba.resize(bt.size());
+        bsrc.resize(bt.size());
+        branch_slots(BT, bt.data() + b0, jv, tr->out_begin, tsys, branch_on, ba.data() + b0, bsrc.data() + b0);
         be.push_back(end);
         bs.push_back(sy);
     }
+    // trunk pre-pass instead of in-workgroup chains: every slot starts at its own branch step from a checkpoint
+    // of its system's MTO-free trunk, which one trajectory per system propagates first. Chosen (PQD_TRUNK=-1,
+    // auto) when the estimated critical path — trunk latency + the longest block from its first activation — is
+    // shorter than the longest block from step 0; PQD_TRUNK=1 forces it, 0 disables it. Needs fused half steps
+    // (checkpoints hold the state with M_b(n-1) deferred).
+    std::vector<int> ca(bt.size(), 0);                 // per slot: activation with a checkpoint (0 = fresh)
+    std::vector<std::vector<int>> ck_steps(n_sys);     // per system: checkpoint steps (sorted, unique)
+    int trunk_mode = -1;
+    if (const char* e = getenv("PQD_TRUNK")) trunk_mode = atoi(e);
+    bool use_trunk = false;
+    if (branch_on && fuse_on && trunk_mode != 0 && ns > 0) {
+        int64_t crit_no = 0, crit_tk = 0, max_ck = 0;
+        const int nbk = (int)be.size();
+        for (int b = 0; b < nbk; ++b) {
+            int start = INT_MAX;
+            for (int q = 0; q < BT; ++q) {
+                const int t = bt[(size_t)b * BT + q];
+                if (t < 0) continue;
+                const int a = std::max(0, std::min(jv[t], tr->out_begin[t]));
+                ca[(size_t)b * BT + q] = a;
+                start = std::min(start, a);
+                if (a >= 1) { ck_steps[tsys[t]].push_back(a); max_ck = std::max<int64_t>(max_ck, a); }
+            }
+            crit_no = std::max<int64_t>(crit_no, be[b]);
+            if (start != INT_MAX) crit_tk = std::max<int64_t>(crit_tk, be[b] - start);
+        }
+        // trunk step latency relative to a lock-step main-sweep step: split groups (N2 >= 9) ~0.5, one batched
+        // workgroup ~0.7
+        const double r = N2 >= 9 ? 0.5 : 0.7;
+        use_trunk = max_ck > 0 && (trunk_mode == 1 || (double)crit_tk + r * (double)max_ck < 0.995 * (double)crit_no);
+    }
+    if (use_trunk) {
+        std::vector<int> ck_base(n_sys, 0);
+        int n_ck = 0;
+        for (int y = 0; y < n_sys; ++y) {
+            auto& v = ck_steps[y];
+            std::sort(v.begin(), v.end());
+            v.erase(std::unique(v.begin(), v.end()), v.end());
+            ck_base[y] = n_ck;
+            n_ck += (int)v.size();
+        }
+        for (size_t i = 0; i < bt.size(); ++i) {
+            const int t = bt[i];
+            if (t < 0) continue;
+            const int a = ca[i];
+            if (a >= 1) {
+                const auto& v = ck_steps[tsys[t]];
+                const int idx = ck_base[tsys[t]] + (int)(std::lower_bound(v.begin(), v.end(), a) - v.begin());
+                ba[i] = a;
+                bsrc[i] = -2 - idx;
+            } else {
+                ba[i] = 0;
+                bsrc[i] = -1;
+            }
+        }
+        if ((rc = plan_trunks(P, ctx, n_sys, ck_steps, ck_base, n_ck, n_cu, N2, n_out, pt, s))) return rc;
+    }
+    for (size_t i = 0; i < bt.size(); ++i)
+        if (bt[i] >= 0) P->traj_steps += tr->out_end[bt[i]] - ba[i] + 1;
     const int nb = (int)be.size();
-    if (bt.empty()) { bt.assign(BT, -1); be.assign(1, 0); bs.assign(1, 0); }
+    if (bt.empty()) { bt.assign(BT, -1); be.assign(1, 0); bs.assign(1, 0); ba.assign(BT, INT_MAX); bsrc.assign(BT, -1); }
     P->n_blocks = nb;
     HIPCHK(P->blk_traj.upload(bt.data(), bt.size(), s));
     HIPCHK(P->blk_end.upload(be.data(), be.size(), s));
     HIPCHK(P->blk_sys.upload(bs.data(), bs.size(), s));
+    HIPCHK(P->blk_act.upload(ba.data(), ba.size(), s));
+    HIPCHK(P->blk_src.upload(bsrc.data(), bsrc.size(), s));
     HIPCHK(P->sched.upload(sch.data(), sch.size(), s));
     HIPCHK(P->out.alloc(std::max<int64_t>(1, out_len)));
     HIPCHK(hipMemsetAsync(P->out.p, 0, std::max<int64_t>(1, out_len) * sizeof(double2), s));
@@ -594,6 +814,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     }
     sp.sched = P->sched.p; sp.rho0 = P->rho0.p; sp.n_out = n_out; sp.ovec = P->ovec.p;
     sp.blk_traj = P->blk_traj.p; sp.blk_end = P->blk_end.p; sp.blk_sys = P->blk_sys.p;
+    sp.blk_act = P->blk_act.p; sp.blk_src = P->blk_src.p;
     sp.traj_sys = P->traj_sys.p; sp.m_stride = (long long)2 * ns * m2; sp.wbeg = P->wbeg.p; sp.wend = P->wend.p;
     { const char* ab = getenv("PQD_ABLATE"); sp.ablate = ab ? atoi(ab) : 0; }
     { const char* b1 = getenv("PQD_SPLIT_B128"); sp.split_b128 = (b1 && atoi(b1) != 0) ? 1 : 0; }
@@ -608,7 +829,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     { const char* c3 = getenv("PQD_CMUL3"); sp.cmul3 = c3 ? atoi(c3) : 1; }
     { const char* tp = getenv("PQD_TRPRE"); sp.trpre = tp ? atoi(tp) : 1; }
     if (pt && (sp.pt_mode == 4 || sp.pt_mode == 5)) {
-        const int nw = P->BT * sweep_wpt(P->BT, P->CHI);
+        const int nw = P->BT * sweep_wpt(P->N2, P->BT, P->CHI);
         int rmax = sweep_rmax(P->N2, P->BT, P->CHI);
         if (const char* e = getenv("PQD_ROWPAIR")) rmax = std::max(1, std::min(rmax, atoi(e) ? rmax : 1));
         std::vector<int4> u = pt_row_units(pt->gmap_h, nw, rmax);
@@ -627,6 +848,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     }
     sp.F = P->F.p; sp.W = P->W.p;
     sp.woff = P->woff.p; sp.ev_start = P->ev_start.p; sp.ev = P->ev.p; sp.sop = P->sop.p; sp.out = P->out.p;
+    finalize_trunks(P);
     if (P->split) {
         HIPCHK(P->Xs.alloc((size_t)P->n_traj * 2 * N2 * P->CHI));
         HIPCHK(P->cnt.alloc((size_t)P->n_traj * 32));
@@ -658,7 +880,7 @@ int pqd_plan_execute(pqd_plan* P, int32_t rebuild_free) {
         if (P->sp.fuse) HIPCHK(launch_fuse_steps(P->N2, P->fu, s));
     }
     HIPCHK(hipEventRecord(e[1], s));
-    HIPCHK(hipMemsetAsync(P->flags.p, 0, sizeof(unsigned), s));
+    HIPCHK(launch_trunks(P, s));
     if (P->nopt)
         HIPCHK(launch_sweep_nopt(P->N2, P->n_traj, P->sp, s));
     else if (P->split)
@@ -682,6 +904,19 @@ int pqd_plan_synchronize(pqd_plan* P) {
     if (!P) return fail(PQD_ERR_ARG, "plan is NULL");
     HIPCHK(hipSetDevice(P->ctx->device));
     hipStream_t s = P->ctx->stream;
+    HIPCHK(hipMemsetAsync(P->flags.p, 0, sizeof(unsigned), s));
+    if (P->n_trunk && P->tk_split) {
+        unsigned err = 0;
+        HIPCHK(hipMemcpyAsync(&err, P->tk_err.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (err) {  // the checkpoints are incomplete: redo the trunks on batched workgroups, then the main sweep
+            P->tk_split = false;
+            P->split_fallbacks++;
+            HIPCHK(hipMemsetAsync(P->tk_err.p, 0, sizeof(unsigned), s));
+            HIPCHK(launch_trunks(P, s));
+            HIPCHK(launch_sweep(P->N2, P->CHI, P->BT, P->n_blocks, P->sp, s));
+        }
+    }
     if (P->split) {
         unsigned err = 0;
         HIPCHK(hipMemcpyAsync(&err, P->err.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
@@ -690,11 +925,11 @@ int pqd_plan_synchronize(pqd_plan* P) {
             P->split = false;
             P->split_fallbacks++;
             HIPCHK(hipMemsetAsync(P->err.p, 0, sizeof(unsigned), s));
-            HIPCHK(hipMemsetAsync(P->flags.p, 0, sizeof(unsigned), s));
             HIPCHK(launch_sweep(P->N2, P->CHI, P->BT, P->n_blocks, P->sp, s));
         }
     }
     unsigned flags = 0;
+    HIPCHK(launch_check_finite(P->out.p, P->out_len, P->flags.p, s));
     HIPCHK(hipMemcpyAsync(&flags, P->flags.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     if (flags & 1u) return fail(PQD_ERR_NUMERIC, "non-finite value (NaN/Inf) in the propagated outputs");
@@ -713,8 +948,9 @@ int pqd_plan_download(pqd_plan* P, pqd_c128* out, int64_t out_len) {
     return rc;  // PQD_ERR_NUMERIC still hands the values over (they show where the run went bad)
 }
 
-int pqd_plan_info(const pqd_plan* P, int32_t* path, int32_t* bt, int32_t* split_fallbacks) {
+int pqd_plan_info(const pqd_plan* P, int32_t* path, int32_t* bt, int32_t* split_fallbacks, int64_t* traj_steps) {
     if (!P) return fail(PQD_ERR_ARG, "plan is NULL");
+    if (traj_steps) *traj_steps = P->traj_steps;
     if (path) *path = P->nopt ? PQD_PATH_NOPT : P->split ? PQD_PATH_SPLIT : PQD_PATH_BATCHED;
     if (bt) *bt = P->BT;
     if (split_fallbacks) *split_fallbacks = P->split_fallbacks;

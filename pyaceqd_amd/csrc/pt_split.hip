@@ -155,8 +155,8 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
             double2 s = c_zero();
 #pragma unroll
             for (int b = 0; b < N2; ++b) c_fma(s, gld(w + (size_t)k * N2 + b), smem[RRO + b]);
-            out_store(p.out + wo + (long long)(n - wb) * p.n_out + k, s, p.flags);
-        }
+                    p.out[wo + (long long)(n - wb) * p.n_out + k] = s;
+                }
     };
     auto has_event = [&](int n) { return ev_cur < ev_lim && p.ev[ev_cur].x == n; };
 
@@ -170,6 +170,12 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
     if (n_end > 0) fetch_slice(0);
     bool pre = false;  // frow holds F(n)[g][tid] of the coming step
     for (int n = 0;; ++n) {
+        // ---- trunk pre-pass: checkpoint of the state at the top of step n (M_b(n-1) still deferred), workgroup 0
+        if (p.ck_map && g == 0 && n >= 1) {
+            const int c = p.ck_map[(size_t)t * p.ck_stride + n];
+            if (c >= 0)
+                for (int e = tid; e < E; e += SP_NT) p.ck[(size_t)c * E + e] = smem[qo + e];
+        }
         // ---- column phase
         const bool fz = p.fuse && n >= 1 && !has_event(n);
         int rb;  // row g of the state the PT contracts

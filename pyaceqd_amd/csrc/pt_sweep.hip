@@ -32,7 +32,7 @@ struct SweepLayout {
     static constexpr int TS = N2 * RS + 4;      // trajectory stride (+64 B: shifts banks per trajectory)
     static constexpr int KD = CHI / 16;         // PT output columns per lane
     static constexpr int NCOL = BT * CHI;       // column-phase work items
-    static constexpr int WPT = sweep_wpt(BT, CHI);  // waves per trajectory
+    static constexpr int WPT = sweep_wpt(N2, BT, CHI);  // waves per trajectory
     static constexpr int NW = BT * WPT;             // waves per workgroup
     static constexpr size_t LDS = (size_t)(BT * TS + BT * N2) * sizeof(double2);
 };
@@ -221,10 +221,12 @@ __device__ __forceinline__ void pt_row_mfma(const double2* __restrict__ Qg, doub
 // R > 1 contracts R Liouville rows that share one PT slice (dictionary PTs: rows with the same
 // coupling-eigenvalue pair) in one pass, so each slice element loaded from L2 feeds R times the MFMAs.
 // a0..a3 = the R row indices (unused ones ignored).
-template <int CHI, int BT, int RS, int TS, int PF = 1, int R = 1>
+// RBN <= BT / 4: only the first RBN row blocks (4 trajectories each) are contracted — the later ones are dormant
+// shared-trunk slots (their rows are left as they are until the slot is activated, pqd_host.cpp branch_slots).
+template <int CHI, int BT, int RS, int TS, int PF = 1, int R = 1, int RBN = BT / 4>
 __device__ __forceinline__ void pt_row_mfma3(const double2* __restrict__ Qg, double2* st, int a0, int a1, int a2,
                                              int a3, int lane) {
-    constexpr int RB = BT / 4, NG = CHI / 16, KSN = CHI / 4;
+    constexpr int RB = RBN, NG = CHI / 16, KSN = CHI / 4;
     const int x = lane & 3, kk = lane >> 4, c16 = lane & 15;
     double p1[R][RB][NG], p2[R][RB][NG], p3[R][RB][NG];
 #pragma unroll
@@ -285,23 +287,31 @@ __device__ __forceinline__ void pt_row_mfma3(const double2* __restrict__ Qg, dou
 }
 
 // a unit of n rows sharing one slice (n <= sweep_rmax: the accumulators stay within 48 doubles)
-template <int N2, int CHI, int BT, int RS, int TS, int PF>
-__device__ __forceinline__ void pt_rows3(const double2* __restrict__ Qg, double2* st, int4 e, int lane) {
+template <int N2, int CHI, int BT, int RS, int TS, int PF, int RBN>
+__device__ __forceinline__ void pt_rows3_n(const double2* __restrict__ Qg, double2* st, int4 e, int lane) {
     constexpr int RM = sweep_rmax(N2, BT, CHI);
     if constexpr (RM >= 4) {
         if (e.w >= 0) {  // rows 2 (and 3) in the low (high) 16 bits of w
             const int a2 = e.w & 0xFFFF, a3 = e.w >> 16;
-            if (a3 != 0x7FFF) pt_row_mfma3<CHI, BT, RS, TS, PF, 4>(Qg, st, e.y, e.z, a2, a3, lane);
-            else pt_row_mfma3<CHI, BT, RS, TS, PF, 3>(Qg, st, e.y, e.z, a2, a2, lane);
+            if (a3 != 0x7FFF) pt_row_mfma3<CHI, BT, RS, TS, PF, 4, RBN>(Qg, st, e.y, e.z, a2, a3, lane);
+            else pt_row_mfma3<CHI, BT, RS, TS, PF, 3, RBN>(Qg, st, e.y, e.z, a2, a2, lane);
             return;
         }
     }
     if constexpr (RM >= 2) {
-        if (e.z >= 0) pt_row_mfma3<CHI, BT, RS, TS, PF, 2>(Qg, st, e.y, e.z, e.z, e.z, lane);
-        else pt_row_mfma3<CHI, BT, RS, TS, PF, 1>(Qg, st, e.y, e.y, e.y, e.y, lane);
+        if (e.z >= 0) pt_row_mfma3<CHI, BT, RS, TS, PF, 2, RBN>(Qg, st, e.y, e.z, e.z, e.z, lane);
+        else pt_row_mfma3<CHI, BT, RS, TS, PF, 1, RBN>(Qg, st, e.y, e.y, e.y, e.y, lane);
     } else {
-        pt_row_mfma3<CHI, BT, RS, TS, PF, 1>(Qg, st, e.y, e.y, e.y, e.y, lane);
+        pt_row_mfma3<CHI, BT, RS, TS, PF, 1, RBN>(Qg, st, e.y, e.y, e.y, e.y, lane);
     }
+}
+
+// all rows of the workgroup, dormant shared-trunk slots included (their rows are overwritten at activation):
+// skipping a dormant row block through a second instance (RBN = 1) cost 0.7% on the bench workload, where blocks
+// are dormant for a few steps only (profiles/r02/ab_rbn.log)
+template <int N2, int CHI, int BT, int RS, int TS, int PF>
+__device__ __forceinline__ void pt_rows3(const double2* __restrict__ Qg, double2* st, int4 e, int lane) {
+    pt_rows3_n<N2, CHI, BT, RS, TS, PF, BT / 4>(Qg, st, e, lane);
 }
 
 // PT contraction of row alpha for BT = 8 on v_mfma_f64_16x16x4_f64 ("split complex"): the 16 MFMA rows are
@@ -347,8 +357,10 @@ __device__ __forceinline__ void pt_row_mfma16(const double2* __restrict__ Qg, do
             wr[(lk + 4 * r) * TS + 16 * t] = make_double2(p1[t][r] - p2[t][r + 2], p2[t][r] + p1[t][r + 2]);
 }
 
-template <int N2, int CHI, int BT>
-__global__ __launch_bounds__(64 * BT * sweep_wpt(BT, CHI)) void pt_sweep_kernel(SweepParams p, const double2* __restrict__ Mg,
+// TRUNK: the trunk pre-pass instance (writes checkpoints through p.ck_map); kept out of the main sweep's instance,
+// where the extra live values cost VGPR spills
+template <int N2, int CHI, int BT, bool TRUNK>
+__global__ __launch_bounds__(64 * BT * sweep_wpt(N2, BT, CHI)) void pt_sweep_kernel(SweepParams p, const double2* __restrict__ Mg,
                                                            const double2* __restrict__ Qg0, double2* __restrict__ outg,
                                                            const double2* __restrict__ Fg, const double2* __restrict__ Wg) {
     using L = SweepLayout<N2, CHI, BT>;
@@ -357,7 +369,7 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(BT, CHI)) void pt_sweep_kernel(
     extern __shared__ __attribute__((aligned(16))) double2 smem[];
     double2* st = smem;
     double2* rbuf = smem + BT * TS;
-    __shared__ int s_traj[BT], s_wb[BT], s_we[BT], s_fz[BT], s_sys[BT];
+    __shared__ int s_traj[BT], s_wb[BT], s_we[BT], s_fz[BT], s_sys[BT], s_act[BT], s_src[BT];
     __shared__ long long s_wo[BT];
 
     const int tid = threadIdx.x;
@@ -373,8 +385,26 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(BT, CHI)) void pt_sweep_kernel(
         s_wo[tid] = t >= 0 ? p.woff[t] : 0;
         s_fz[tid] = 0;
         s_sys[tid] = t >= 0 ? p.traj_sys[t] : 0;
+        s_act[tid] = p.blk_act[blockIdx.x * BT + tid];
+        s_src[tid] = p.blk_src[blockIdx.x * BT + tid];
     }
     __syncthreads();
+    // shared trunk (pqd_host.cpp branch_slots): a slot is dormant before its activation step, then copies the
+    // (state, fused flag) of an earlier-activated slot of its workgroup or a trunk checkpoint. next_act: the next step
+    // with activations
+    const int my_act = __builtin_amdgcn_readfirstlane(s_act[tw]);
+    auto next_activation = [&](int after) {
+        int m = INT_MAX;
+#pragma unroll
+        for (int b = 0; b < BT; ++b)
+            if (s_act[b] > after && s_act[b] < m) m = s_act[b];
+        return m;
+    };
+    int n0 = INT_MAX;  // first step of the block: its earliest activation (0 unless every slot starts later)
+#pragma unroll
+    for (int b = 0; b < BT; ++b) n0 = s_act[b] < n0 ? s_act[b] : n0;
+    if (n0 == INT_MAX) return;  // no trajectory in this workgroup (the whole block exits together)
+    int next_act = n0 > 0 ? n0 : next_activation(0);
     const int n_end = p.blk_end[blockIdx.x];
     // a workgroup may mix systems (per-trajectory drives, e.g. one system per scan point): each wave reads the
     // free propagators of its own trajectory's system
@@ -419,8 +449,53 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(BT, CHI)) void pt_sweep_kernel(
     const int ntr = BT * p.n_out * N2;
     const bool lanetr = (N2 == 4 || N2 == 16) && p.trpre && ntr <= NT;
     double2 wpre = c_zero();
+    if (n0 > 0 && lanetr && tid < ntr) {  // the step the loop starts at: W(n0) row element, as fetched a step ahead
+        const int a = tid % N2, bk = tid / N2, b = bk / p.n_out, k = bk - (bk / p.n_out) * p.n_out;
+        wpre = Wg[(size_t)s_sys[b] * p.w_stride + ((size_t)n0 * p.n_out + k) * N2 + a];
+    }
     bool fz = false;  // this wave's trajectory sits between M_b(n-1) and M_a(n) unapplied (fused step n)
-    for (int n = 0;; ++n) {
+    for (int n = n0;; ++n) {
+        // ------------------------------------------------------------ shared-trunk activations at step n
+        if (n == next_act) {
+            // a checkpoint (src <= -2) holds the trunk at the top of step n >= 1 with M_b(n-1) deferred (fused)
+            if (tid < BT && s_act[tid] == n) s_fz[tid] = s_src[tid] >= 0 ? s_fz[s_src[tid]] : 1;
+            for (int b = 0; b < BT; ++b) {
+                if (s_act[b] != n) continue;
+                double2* dp = st + b * TS;
+                if (s_src[b] >= 0) {
+                    const double2* sp = st + s_src[b] * TS;
+                    for (int e = tid; e < N2 * CHI; e += NT) {
+                        const int a = e / CHI, c = e - (e / CHI) * CHI;
+                        dp[a * RS + c] = sp[a * RS + c];
+                    }
+                } else if (s_src[b] <= -2) {
+                    const double2* cp = p.ck + (size_t)(-2 - s_src[b]) * N2 * CHI;
+                    for (int e = tid; e < N2 * CHI; e += NT) {
+                        const int a = e / CHI, c = e - (e / CHI) * CHI;
+                        dp[a * RS + c] = cp[e];
+                    }
+                }
+            }
+            if (my_act == n) fz = s_src[tw] >= 0 ? (s_fz[s_src[tw]] != 0) : true;
+            next_act = next_activation(n);
+            __syncthreads();
+        }
+        // ------------------------------------------------------------ trunk pre-pass: checkpoints at step n
+        if constexpr (TRUNK) {
+            bool wrote = false;
+            for (int b = 0; b < BT; ++b) {
+                const int t = s_traj[b];
+                const int c = t >= 0 ? p.ck_map[(size_t)t * p.ck_stride + n] : -1;
+                if (c < 0) continue;
+                wrote = true;
+                double2* cp = p.ck + (size_t)c * N2 * CHI;
+                for (int e = tid; e < N2 * CHI; e += NT) {
+                    const int a = e / CHI, cc = e - (e / CHI) * CHI;
+                    cp[e] = st[b * TS + a * RS + cc];
+                }
+            }
+            if (wrote) __syncthreads();
+        }
         // ------------------------------------------------------------ outputs at step n
         bool need = false;
 #pragma unroll
@@ -452,7 +527,7 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(BT, CHI)) void pt_sweep_kernel(
 #pragma unroll
                     for (int m = 1; m < N2; m <<= 1) x = c_add(x, c_shfl_xor(x, m));
                     if (a == 0 && s_wb[b] <= n && n <= s_we[b])
-                        out_store(outg + s_wo[b] + (long long)(n - s_wb[b]) * p.n_out + k, x, p.flags);
+                        outg[s_wo[b] + (long long)(n - s_wb[b]) * p.n_out + k] = x;
                 }
             } else
             for (int e = tid; e < BT * p.n_out; e += NT) {
@@ -475,7 +550,7 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(BT, CHI)) void pt_sweep_kernel(
                         for (int j = 0; j < CK; ++j)
                             if (a0 + j < N2) c_fma(s, ovr[j], rbuf[b * N2 + a0 + j]);
                     }
-                    out_store(outg + s_wo[b] + (long long)(n - s_wb[b]) * p.n_out + k, s, p.flags);
+                    outg[s_wo[b] + (long long)(n - s_wb[b]) * p.n_out + k] = s;
                 }
             }
         }
@@ -487,10 +562,13 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(BT, CHI)) void pt_sweep_kernel(
 
         // ------------------------------------------------------------ column phase A
         const double2* Ma = Mg + (size_t)(2 * n) * N2 * N2;
-        if (!(p.ablate & 2)) {
-            if (fz) {  // no MTO at step n: M_b(n-1) and M_a(n) in one operator
+        if (!(p.ablate & 2) && n >= my_act) {
+            const bool mto_now = ev_cur < ev_lim && p.ev[ev_cur].x == n;
+            if (fz && !mto_now) {  // no MTO at step n: M_b(n-1) and M_a(n) in one operator
                 col(Fg + (size_t)n * N2 * N2);
             } else {
+                // a slot activated at n holds the trunk's state with M_b(n-1) still deferred, but has an MTO at n
+                if (fz) col(Mg + (size_t)(2 * n - 1) * N2 * N2);
                 while (ev_cur < ev_lim) {  // applyBefore-false MTOs at step n
                     const int4 e = p.ev[ev_cur];
                     if (e.x != n || e.y != 1) break;
@@ -617,7 +695,7 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(BT, CHI)) void pt_sweep_kernel(
         const double2* Mb = Ma + N2 * N2;
         // fuse M_b(n) into the next step's operator unless this trajectory has an MTO at step n+1
         fz = p.fuse && !(ev_cur < ev_lim && p.ev[ev_cur].x == n + 1);
-        if (!(p.ablate & 2) && !fz) {
+        if (!(p.ablate & 2) && !fz && n >= my_act) {
             col(Mb);
             while (ev_cur < ev_lim) {  // applyBefore-true MTOs at step n+1
                 const int4 e = p.ev[ev_cur];
@@ -675,7 +753,7 @@ __global__ __launch_bounds__(64) void sweep_nopt_kernel(SweepParams p) {
                 const double2* ov = p.ovec + (size_t)k * N2;
 #pragma unroll
                 for (int a = 0; a < N2; ++a) c_fma(s, ov[a], x[a]);
-                out_store(p.out + wo + (long long)(n - wb) * p.n_out + k, s, p.flags);
+                p.out[wo + (long long)(n - wb) * p.n_out + k] = s;
             }
         }
         if (n >= we) break;
@@ -697,31 +775,31 @@ __global__ __launch_bounds__(64) void sweep_nopt_kernel(SweepParams p) {
     }
 }
 
-template <int N2, int CHI, int BT>
+template <int N2, int CHI, int BT, bool TRUNK>
 hipError_t launch_sw(int n_blocks, const SweepParams& p, hipStream_t s) {
     using L = SweepLayout<N2, CHI, BT>;
     static_assert(L::LDS <= 160 * 1024, "LDS budget");
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)pt_sweep_kernel<N2, CHI, BT>,
+        hipError_t e = hipFuncSetAttribute((const void*)pt_sweep_kernel<N2, CHI, BT, TRUNK>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::LDS);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((pt_sweep_kernel<N2, CHI, BT>), dim3(n_blocks), dim3(64 * L::NW), L::LDS, s, p, p.M, p.Q, p.out,
-                       p.F, p.W);
+    hipLaunchKernelGGL((pt_sweep_kernel<N2, CHI, BT, TRUNK>), dim3(n_blocks), dim3(64 * L::NW), L::LDS, s, p, p.M, p.Q,
+                       p.out, p.F, p.W);
     return hipGetLastError();
 }
 
-template <int N2, int BT>
+template <int N2, int BT, bool TRUNK = false>
 hipError_t launch_sw_chi(int CHI, int n_blocks, const SweepParams& p, hipStream_t s) {
     switch (CHI) {
-        case 16: return launch_sw<N2, 16, BT>(n_blocks, p, s);
-        case 32: return launch_sw<N2, 32, BT>(n_blocks, p, s);
-        case 64: return launch_sw<N2, 64, BT>(n_blocks, p, s);
+        case 16: return launch_sw<N2, 16, BT, TRUNK>(n_blocks, p, s);
+        case 32: return launch_sw<N2, 32, BT, TRUNK>(n_blocks, p, s);
+        case 64: return launch_sw<N2, 64, BT, TRUNK>(n_blocks, p, s);
         case 128:
             // chi = 128 keeps 4 augmented states of N2 <= 16 in LDS (132 KiB); larger N2 or BT do not fit
-            if constexpr (BT == 4 && N2 <= 16) return launch_sw<N2, 128, BT>(n_blocks, p, s);
+            if constexpr (BT == 4 && N2 <= 16) return launch_sw<N2, 128, BT, TRUNK>(n_blocks, p, s);
             return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
     }
@@ -739,6 +817,17 @@ int sweep_max_bt(int N2) { return N2 <= 16 ? 8 : 4; }
 
 hipError_t launch_sweep(int N2, int CHI, int BT, int n_blocks, const SweepParams& p, hipStream_t s) {
     if (n_blocks <= 0) return hipSuccess;
+    if (p.ck_map) {  // trunk pre-pass: four trunks per workgroup
+        if (BT != 4) return hipErrorInvalidValue;
+        switch (N2) {
+            case 4: return launch_sw_chi<4, 4, true>(CHI, n_blocks, p, s);
+            case 9: return launch_sw_chi<9, 4, true>(CHI, n_blocks, p, s);
+            case 16: return launch_sw_chi<16, 4, true>(CHI, n_blocks, p, s);
+            case 25: return launch_sw_chi<25, 4, true>(CHI, n_blocks, p, s);
+            case 36: return launch_sw_chi<36, 4, true>(CHI, n_blocks, p, s);
+            default: return hipErrorInvalidValue;
+        }
+    }
     if (BT == 8) {
         switch (N2) {
             case 4: return launch_sw_chi<4, 8>(CHI, n_blocks, p, s);

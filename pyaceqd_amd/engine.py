@@ -297,9 +297,15 @@ class Plan:
 
     def info(self):
         """(path name, trajectories per workgroup, split launches that fell back to the batched kernel)"""
-        p, b, f = C.c_int32(), C.c_int32(), C.c_int32()
-        _lib.check(_lib.lib().pqd_plan_info(self.handle, C.byref(p), C.byref(b), C.byref(f)))
+        p, b, f, n = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int64()
+        _lib.check(_lib.lib().pqd_plan_info(self.handle, C.byref(p), C.byref(b), C.byref(f), C.byref(n)))
         return self.PATHS[p.value], b.value, f.value
+
+    def traj_steps(self):
+        """trajectory-steps one execute propagates (shared trunks counted once per workgroup)"""
+        p, b, f, n = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int64()
+        _lib.check(_lib.lib().pqd_plan_info(self.handle, C.byref(p), C.byref(b), C.byref(f), C.byref(n)))
+        return n.value
 
     def output_device_ptr(self):
         return _lib.lib().pqd_plan_output_device(self.handle)
