@@ -32,6 +32,21 @@ __device__ __forceinline__ double2 sample_ch(const FreePropSys& p, int c, double
     return make_double2(a.x + w * (b.x - a.x), a.y + w * (b.y - a.y));
 }
 
+// a half step is idle when every channel sample at every sub-step midpoint is exactly zero: then
+// L(t) = L0 + 0 S + 0 T is bitwise L0, and its propagator is the system's Midle (built by the idle pass with the
+// same code and zero samples), so it is copied instead of recomputed. Pulses are localised: the TLS scans
+//  have zero drive after ~135 ps of a 100/1000 ps window.
+__device__ __forceinline__ bool idle_half_step(const FreePropSys& sy, double t0, double w, int nsub) {
+    for (int j = 0; j < nsub; ++j) {
+        const double t = t0 + (j + 0.5) * w;
+        for (int c = 0; c < sy.n_chan && c < 4; ++c) {
+            const double2 f = sample_ch(sy, c, t);
+            if (f.x != 0.0 || f.y != 0.0) return false;
+        }
+    }
+    return true;
+}
+
 template <int N2>
 __device__ __forceinline__ void lds_matmul(const double2* A, const double2* B, double2* C, int tid) {
     if constexpr (N2 == 36) {
@@ -83,22 +98,31 @@ __global__ __launch_bounds__(256) void free_prop_kernel(FreePropParams p) {
     __shared__ int s_sh, s_deg;
 
     const int tid = threadIdx.x;
-    const long long nblk = (long long)p.n_sys * 2 * p.n_steps;
+    const long long nblk = p.idle_pass ? (long long)p.n_sys : (long long)p.n_sys * 2 * p.n_steps;
     // grid-stride: the dispatch grid counts work-items in 32 bits, so a launch is capped (FP_MAX_BLOCKS)
     for (long long blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-    const int si = (int)(blk / (2 * p.n_steps));
-    const int m = (int)(blk - (long long)si * 2 * p.n_steps);
+    const int si = p.idle_pass ? (int)blk : (int)(blk / (2 * p.n_steps));
+    const int m = p.idle_pass ? 0 : (int)(blk - (long long)si * 2 * p.n_steps);
     const int n = m >> 1, h = m & 1;
     const FreePropSys sy = p.systems[si];
     const int nsub = p.n_sub > 0 ? p.n_sub : 1;
     const double w = 0.5 * p.dt / nsub;
+    double2* out = p.idle_pass ? p.Midle + (size_t)si * N2 * N2 : p.M + ((size_t)si * 2 * p.n_steps + m) * N2 * N2;
+    if (!p.idle_pass && p.Midle && idle_half_step(sy, p.ta + n * p.dt + h * 0.5 * p.dt, w, nsub)) {
+        const double2* src = p.Midle + (size_t)si * N2 * N2;
+        for (int e = tid; e < N2 * N2; e += 256) out[e] = src[e];
+        continue;  // block-uniform: LDS untouched
+    }
 
     for (int j = 0; j < nsub; ++j) {
         const double t = p.ta + n * p.dt + h * 0.5 * p.dt + (j + 0.5) * w;
         double2 f[4], fc[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            if (c < sy.n_chan) { f[c] = sample_ch(sy, c, t); fc[c] = c_conj(f[c]); }
+            if (c < sy.n_chan) {
+                f[c] = p.idle_pass ? c_zero() : sample_ch(sy, c, t);
+                fc[c] = c_conj(f[c]);
+            }
         }
         for (int e = tid; e < N2 * N2; e += 256) {
             double2 v = sy.L0[e];
@@ -172,7 +196,6 @@ __global__ __launch_bounds__(256) void free_prop_kernel(FreePropParams p) {
         }
         __syncthreads();
     }
-    double2* out = p.M + ((size_t)si * 2 * p.n_steps + m) * N2 * N2;
     const double2* res = (nsub == 1) ? P : Acc;
     for (int e = tid; e < N2 * N2; e += 256) out[e] = res[e];
     __syncthreads();  // Acc is rewritten by the next matrix
@@ -199,24 +222,31 @@ __device__ __forceinline__ double2 grp_matmul4(double2 a, double2 b, int gb, int
 
 __global__ __launch_bounds__(256) void free_prop4_kernel(FreePropParams p) {
     const int tid = threadIdx.x;
-    const long long n_mat = (long long)p.n_sys * 2 * p.n_steps;
+    const long long n_mat = p.idle_pass ? (long long)p.n_sys : (long long)p.n_sys * 2 * p.n_steps;
     for (long long base = (long long)blockIdx.x * 16; base < n_mat; base += (long long)gridDim.x * 16) {
     const long long mat = base + (tid >> 4);
     const bool live = mat < n_mat;
     const long long mc = live ? mat : n_mat - 1;  // dead lanes shadow the last matrix (no store)
-    const int si = (int)(mc / (2 * p.n_steps));
-    const int m = (int)(mc - (long long)si * 2 * p.n_steps);
+    const int si = p.idle_pass ? (int)mc : (int)(mc / (2 * p.n_steps));
+    const int m = p.idle_pass ? 0 : (int)(mc - (long long)si * 2 * p.n_steps);
     const int n = m >> 1, h = m & 1;
     const int lane = tid & 63, gb = lane & ~15, e = lane & 15, i = e >> 2, j = e & 3;
     const FreePropSys sy = p.systems[si];
     const int nsub = p.n_sub > 0 ? p.n_sub : 1;
     const double w = 0.5 * p.dt / nsub;
+    double2* out = p.idle_pass ? p.Midle + (size_t)si * 16 : p.M + ((size_t)si * 2 * p.n_steps + m) * 16;
+    // an idle half step copies Midle; the test is uniform within the 16-lane group (one matrix), so the group's
+    // shuffles below never mix copied and computed matrices of different groups
+    if (!p.idle_pass && p.Midle && idle_half_step(sy, p.ta + n * p.dt + h * 0.5 * p.dt, w, nsub)) {
+        if (live) out[e] = p.Midle[(size_t)si * 16 + e];
+        continue;
+    }
     double2 acc = c_zero();
     for (int js = 0; js < nsub; ++js) {
         const double t = p.ta + n * p.dt + h * 0.5 * p.dt + (js + 0.5) * w;
         double2 v = sy.L0[e];
         for (int c = 0; c < sy.n_chan && c < 4; ++c) {
-            const double2 f = sample_ch(sy, c, t);
+            const double2 f = p.idle_pass ? c_zero() : sample_ch(sy, c, t);
             c_fma(v, f, sy.S[(size_t)c * 16 + e]);
             c_fma(v, c_conj(f), sy.T[(size_t)c * 16 + e]);
         }
@@ -246,7 +276,7 @@ __global__ __launch_bounds__(256) void free_prop4_kernel(FreePropParams p) {
         for (int q = 0; q < sh; ++q) pm = grp_matmul4(pm, pm, gb, i, j);
         acc = (js == 0) ? pm : grp_matmul4(pm, acc, gb, i, j);
     }
-    if (live) p.M[((size_t)si * 2 * p.n_steps + m) * 16 + e] = acc;
+    if (live) out[e] = acc;
     }
 }
 
@@ -260,7 +290,7 @@ hipError_t launch_fp(const FreePropParams& p, hipStream_t s) {
         if (e != hipSuccess) return e;
         attr = true;
     }
-    const long long nblk = 2LL * p.n_steps * p.n_sys;
+    const long long nblk = p.idle_pass ? (long long)p.n_sys : 2LL * p.n_steps * p.n_sys;
     if (nblk <= 0) return hipSuccess;
     // A, P, T (+ Acc only for n_sub > 1): at N2 = 36, 62 KiB instead of 83 KiB lets two workgroups share a CU
     const size_t lds_run = (p.n_sub > 1 ? 4ull : 3ull) * N2 * N2 * sizeof(double2);
@@ -302,10 +332,45 @@ __global__ __launch_bounds__(256) void fuse_steps_kernel(FuseParams p) {
     }
 }
 
+// small N2: one thread per output element of every (system, step) — F(m) entries, then W(m) entries — instead of a
+// 256-thread workgroup per step with N2^2 + n_out N2 of its threads busy (N2 = 4: 24 of 256)
+template <int N2>
+__global__ __launch_bounds__(256) void fuse_steps_flat_kernel(FuseParams p) {
+    const int E = N2 * N2 + p.n_out * N2;
+    const long long total = (long long)p.n_sys * p.n_steps * E;
+    for (long long idx = (long long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
+        const long long blk = idx / E;
+        const int e = (int)(idx - blk * E);
+        const int si = (int)(blk / p.n_steps), m = (int)(blk - (long long)si * p.n_steps) + 1;
+        const double2* Mb = p.M + ((size_t)si * 2 * p.n_steps + 2 * (m - 1) + 1) * N2 * N2;
+        double2 acc = c_zero();
+        if (e < N2 * N2) {
+            if (m >= p.n_steps) continue;
+            const double2* Ma = p.M + ((size_t)si * 2 * p.n_steps + 2 * m) * N2 * N2;
+            const int r = e / N2, c = e - (e / N2) * N2;
+#pragma unroll
+            for (int k = 0; k < N2; ++k) c_fma(acc, Ma[r * N2 + k], Mb[k * N2 + c]);
+            p.F[((size_t)si * p.n_steps + m) * N2 * N2 + e] = acc;
+        } else {
+            const int q = e - N2 * N2, k = q / N2, a = q - (q / N2) * N2;
+#pragma unroll
+            for (int b = 0; b < N2; ++b) c_fma(acc, p.ovec[k * N2 + b], Mb[b * N2 + a]);
+            p.W[((size_t)si * (p.n_steps + 1) + m) * p.n_out * N2 + q] = acc;
+        }
+    }
+}
+
 template <int N2>
 hipError_t launch_fs(const FuseParams& p, hipStream_t s) {
     const long long nblk = (long long)p.n_sys * p.n_steps;
     if (nblk <= 0) return hipSuccess;
+    if constexpr (N2 <= 9) {
+        const long long total = nblk * (N2 * N2 + p.n_out * N2);
+        hipLaunchKernelGGL(fuse_steps_flat_kernel<N2>, dim3((unsigned)std::min<long long>((total + 255) / 256,
+                                                                                          FP_MAX_BLOCKS)),
+                           dim3(256), 0, s, p);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(fuse_steps_kernel<N2>, dim3((unsigned)std::min<long long>(nblk, FP_MAX_BLOCKS)), dim3(256), 0,
                        s, p);
     return hipGetLastError();
@@ -324,9 +389,9 @@ hipError_t launch_fuse_steps(int N2, const FuseParams& p, hipStream_t s) {
     }
 }
 
-hipError_t launch_free_prop(int N2, const FreePropParams& p, hipStream_t s) {
+static hipError_t launch_free_prop_pass(int N2, const FreePropParams& p, hipStream_t s) {
     if (N2 == 4 && p.packed4) {  // packed4 = 0 (PQD_FP4=0 at plan creation): the general kernel (A/B)
-        const long long n_mat = (long long)p.n_sys * 2 * p.n_steps;
+        const long long n_mat = p.idle_pass ? (long long)p.n_sys : (long long)p.n_sys * 2 * p.n_steps;
         if (n_mat <= 0) return hipSuccess;
         hipLaunchKernelGGL(free_prop4_kernel, dim3((unsigned)std::min<long long>((n_mat + 15) / 16, FP_MAX_BLOCKS)),
                            dim3(256), 0, s, p);
@@ -340,4 +405,16 @@ hipError_t launch_free_prop(int N2, const FreePropParams& p, hipStream_t s) {
         case 36: return launch_fp<36>(p, s);
         default: return hipErrorInvalidValue;
     }
+}
+
+// with p.Midle: the idle propagators first (one per system), then every half step (idle ones copy Midle)
+hipError_t launch_free_prop(int N2, const FreePropParams& p, hipStream_t s) {
+    FreePropParams q = p;
+    if (p.Midle && p.n_steps > 0) {
+        q.idle_pass = 1;
+        hipError_t e = launch_free_prop_pass(N2, q, s);
+        if (e != hipSuccess) return e;
+    }
+    q.idle_pass = 0;
+    return launch_free_prop_pass(N2, q, s);
 }

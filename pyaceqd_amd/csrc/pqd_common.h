@@ -46,6 +46,9 @@ struct FreePropParams {
     int n_steps, n_sub;
     double2* M;              // out: n_sys*2*n_steps*N2*N2
     int packed4;             // N2 = 4: 16 matrices per workgroup (free_prop4_kernel); 0: the general kernel (A/B)
+    double2* Midle;          // n_sys*N2*N2: exp(L0 w)^n_sub, the propagator of a half step whose pulse samples are all
+                             //   exactly zero (built first, copied for every such half step); NULL: always compute
+    int idle_pass;           // 1: this launch builds Midle (one matrix per system, samples taken as 0)
 };
 
 struct SweepParams {

@@ -208,7 +208,7 @@ struct pqd_plan {
     bool split = false;  // small batch: one trajectory over N2 workgroups (pt_split.hip)
     DevBuf<double2> Xs;
     DevBuf<unsigned> cnt, err;
-    DevBuf<double2> L0, S, T, samples, M, F, W, rho0, ovec, sop, out;
+    DevBuf<double2> L0, S, T, samples, M, Midle, F, W, rho0, ovec, sop, out;
     DevBuf<FreePropSys> systab;
     FuseParams fu{};
     DevBuf<int> sched, blk_traj, blk_end, blk_sys, blk_act, blk_src, traj_sys, wbeg, wend, ev_start;
@@ -375,7 +375,7 @@ int pqd_free_propagators(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* gr
     if ((rc = check_grid(grid))) return rc;
     HIPCHK(hipSetDevice(ctx->device));
     const int N2 = sys->dim * sys->dim;
-    DevBuf<double2> L0, S, T, smp, M;
+    DevBuf<double2> L0, S, T, smp, M, Mi;
     DevBuf<FreePropSys> tab;
     hipStream_t s = ctx->stream;
     if ((rc = upload_systems(1, sys, s, L0, S, T, smp, tab))) return rc;
@@ -385,6 +385,10 @@ int pqd_free_propagators(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* gr
     fp.systems = tab.p; fp.n_sys = 1;
     fp.ta = grid->ta; fp.dt = grid->dt; fp.n_steps = grid->n_steps; fp.n_sub = grid->n_sub; fp.M = M.p;
     { const char* f4 = getenv("PQD_FP4"); fp.packed4 = (f4 && atoi(f4) == 0) ? 0 : 1; }
+    if (const char* ie = getenv("PQD_IDLE"); !(ie && atoi(ie) == 0)) {
+        HIPCHK(Mi.alloc((size_t)N2 * N2));
+        fp.Midle = Mi.p;
+    }
     HIPCHK(launch_free_prop(N2, fp, s));
     if (nM) HIPCHK(hipMemcpyAsync(M_out, M.p, nM * sizeof(double2), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -804,6 +808,10 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     HIPCHK(hipMemsetAsync(P->out.p, 0, std::max<int64_t>(1, out_len) * sizeof(double2), s));
 
     P->fp.systems = P->systab.p; P->fp.n_sys = n_sys;
+    if (const char* ie = getenv("PQD_IDLE"); !(ie && atoi(ie) == 0)) {  // PQD_IDLE=0: compute every half step (A/B)
+        HIPCHK(P->Midle.alloc((size_t)n_sys * m2));
+        P->fp.Midle = P->Midle.p;
+    }
     P->fp.ta = grid->ta; P->fp.dt = grid->dt; P->fp.n_steps = ns; P->fp.n_sub = grid->n_sub; P->fp.M = P->M.p;
 
     SweepParams& sp = P->sp;

@@ -132,3 +132,28 @@ def test_plan_timing_ring_bounded():
     assert n == 64 and f >= 0 and w >= 0
     plan.execute()
     assert plan.timing(reset=False)[2] == 1
+
+
+@pytest.mark.parametrize("N,n_sub", [(2, 1), (2, 2), (3, 1), (4, 1), (6, 1)])
+def test_idle_half_steps_copy_the_idle_propagator(monkeypatch, N, n_sub):
+    """half steps whose pulse samples are all exactly zero copy exp(L0 w)^n_sub (built once per system): same
+    values as computing them (PQD_IDLE=0), and the oracle's"""
+    sysd, grid = H.random_system(N, n_steps=40, n_sub=n_sub, seed=7 + N)
+    chans = []
+    for X, f in sysd.channels:
+        f = np.array(f)
+        f[: len(f) // 4] = 0.0          # drive off at the start ...
+        f[len(f) // 2:] = 0.0           # ... and after the middle
+        chans.append((X, f))
+    sysd.channels = chans
+    got = engine.free_propagators(sysd, grid)
+    assert rel(got, oracle.free_propagators(sysd, grid)) < 1e-12
+    monkeypatch.setenv("PQD_IDLE", "0")
+    assert np.array_equal(got, engine.free_propagators(sysd, grid))
+    tr = Trajectories(np.array([0, 3]), np.array([40, 38]), [MTO(1, 25, False, 1, H.ketbra(N, 1, 0))])
+    ops = [H.ketbra(N, 1, 1), H.ketbra(N, 0, 1)]
+    rho0 = H.random_rho(N)
+    ref = oracle.propagate(sysd, grid, rho0, ops, tr)
+    monkeypatch.setenv("PQD_IDLE", "1")
+    for a, b in zip(engine.propagate(sysd, grid, rho0, ops, tr), ref):
+        assert rel(a, b) < 1e-12
