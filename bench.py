@@ -102,6 +102,21 @@ def pmc_traffic(cfg):
     return float(rec["hbm_bytes_per_launch"]), "profiles/pmc_traffic.json (" + rec.get("passes", "") + ")"
 
 
+def pmc_mfma(cfg):
+    """executed FP64 MFMA flop per sweep launch and the MFMA-busy fraction from the committed SQ counter pass
+    (profiles/pmc_mfma.json: SQ_INSTS_VALU_MFMA_MOPS_F64 x 512, SQ_VALU_MFMA_BUSY_CYCLES over 1024 SIMDs) when it
+    was measured on this exact workload; None otherwise"""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_mfma.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if any(rec.get("config", {}).get(k) != v for k, v in cfg.items()):
+        return None
+    return rec
+
+
 def host_cpu():
     """what the CPU baseline runs on: model, logical CPUs of the machine, CPUs this process may use (affinity and
     cgroup quota), and whether the reference's ACE binary exists here"""
@@ -239,8 +254,10 @@ def main():
     fused = os.environ.get("PQD_FUSE", "1") != "0"
     F = flops_per_traj_step(4, args.chi, len(ops), fused=fused)
     achieved_tf = executed * F / (ms_sweep * 1e-3) / 1e12
-    traffic, traffic_src = pmc_traffic({"n_tau": args.n_tau, "traj_per_gpu": n_traj, "chi": args.chi,
-                                        "scan_points_per_gpu": args.scan, "t1_points": args.t1})
+    wl = {"n_tau": args.n_tau, "traj_per_gpu": n_traj, "chi": args.chi, "scan_points_per_gpu": args.scan,
+          "t1_points": args.t1}
+    traffic, traffic_src = pmc_traffic(wl)
+    mf = pmc_mfma(wl)
     line = {
         "metric": "propagation steps/sec (whole node), 4-level biexciton PT bond-dim 64",
         "value": value,
@@ -271,6 +288,15 @@ def main():
                      "hbm_algorithmic_GBs": bytes_per_launch(grid.n_steps, 410, args.chi, n_traj=n_traj,
                                                              executed_steps=executed) / (ms_sweep * 1e-3) / 1e9},
     }
+    if mf is not None:
+        # what the matrix cores actually execute (3M products: 6 real flops per complex MAC), from the counters,
+        # priced against this run's kernel time
+        line["roofline"]["executed_mfma"] = {
+            "flop_per_launch": mf["executed_mfma_flop"],
+            "TFLOPs": mf["executed_mfma_flop"] / (ms_sweep * 1e-3) / 1e12,
+            "frac": mf["executed_mfma_flop"] / (ms_sweep * 1e-3) / 1e12 / PEAK_FP64_TFLOPS,
+            "mfma_busy_frac": mf["mfma_busy_frac"], "effective_clock_GHz": mf["effective_clock_GHz"],
+            "source": mf["source"]}
     if rank == 0 and world == 1:
         # the reference's single-run case (one trajectory of the same model, chi and length; outside the timed
         # region): a latency figure, carried by N2 split workgroups

@@ -14,5 +14,8 @@ fi
 [[ $STEPS == *fetch* ]] && run pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc/fetch -o run --output-format csv -- python bench.py $ARGS
 [[ $STEPS == *write* ]] && run pmc_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc/write -o run --output-format csv -- python bench.py $ARGS
 [[ $STEPS == *sq* ]] && run pmc_sq 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES -d gpurun_out/pmc/sq -o run --output-format csv -- python bench.py $ARGS
+[[ $STEPS == *list* ]] && run pmc_list 120 rocprofv3 -L
+# executed-MFMA evidence for the headline kernel: FP64 MFMA ops, MFMA-busy cycles, SQ busy, clock
+[[ $STEPS == *mfma* ]] && run pmc_mfma 600 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT -d gpurun_out/pmc/mfma -o run --output-format csv -- python bench.py $ARGS
 find gpurun_out/pmc -name "*counter_collection*.csv" | head
 exit 0
