@@ -149,6 +149,7 @@ int pqd_plan_download(pqd_plan* plan, pqd_c128* out, int64_t out_len);
 #define PQD_PATH_NOPT 0     /* no PT: one wave per trajectory */
 #define PQD_PATH_BATCHED 1  /* lock-step PT sweep, bt trajectories per workgroup */
 #define PQD_PATH_SPLIT 2    /* one trajectory over N^2 workgroups (latency path) */
+#define PQD_PATH_QUAD 3     /* two-level system: four trajectories per wave set, state in registers (pt_quad.hip) */
 /* the path the plan runs now, its trajectories per workgroup, how many split launches fell back, and the
  * trajectory-steps one execute propagates (trajectories of one system that share a lock-step workgroup propagate
  * their common MTO-free trunk once: PQD_BRANCH) */

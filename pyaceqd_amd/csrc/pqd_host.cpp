@@ -206,6 +206,8 @@ struct pqd_plan {
     int N2 = 0, CHI = 1, BT = 4, n_traj = 0, n_blocks = 0, n_steps = 0, n_sys = 1;
     bool nopt = true;
     bool split = false;  // small batch: one trajectory over N2 workgroups (pt_split.hip)
+    bool quad = false;   // two-level system: register-resident quads (pt_quad.hip), blocks of BT = 4
+    int qpw = 2;         // quads per workgroup (PQD_QPW)
     DevBuf<double2> Xs;
     DevBuf<unsigned> cnt, err;
     DevBuf<double2> L0, S, T, samples, M, Midle, F, W, rho0, ovec, sop, out;
@@ -547,6 +549,12 @@ static void finalize_trunks(pqd_plan* P) {
     k.umax = (int)(P->tk_units.n / nw);
 }
 
+// the main batched sweep of a plan: quads (N2 = 4) or BT-trajectory workgroups
+static hipError_t launch_main(pqd_plan* P, hipStream_t s) {
+    if (P->quad) return launch_quad(P->CHI, P->n_blocks, P->qpw, P->sp, s);
+    return launch_sweep(P->N2, P->CHI, P->BT, P->n_blocks, P->sp, s);
+}
+
 static hipError_t launch_trunks(pqd_plan* P, hipStream_t s) {
     if (!P->n_trunk) return hipSuccess;
     if (P->tk_split) return launch_split(P->N2, P->CHI, P->n_trunk, P->tk, P->tk_Xs.p, P->tk_cnt.p, P->tk_err.p, s);
@@ -705,6 +713,14 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     int BT = (sweep_max_bt(N2) >= 8 && tr->n_traj >= 8 * n_cu) ? 8 : 4;
     if (const char* e = getenv("PQD_BT")) BT = std::min(atoi(e) >= 8 ? 8 : 4, sweep_max_bt(N2));
     if (P->CHI > 64) BT = 4;  // chi = 128: only four augmented states fit the LDS
+    // two-level system: the register-resident quad kernel (pt_quad.hip) unless split groups were forced or
+    // PQD_QUAD=0 (A/B); its blocks are quads
+    {
+        const char* e = getenv("PQD_QUAD");
+        P->quad = pt && !P->split && quad_supported(N2, P->CHI) && !(e && atoi(e) == 0);
+        if (const char* w = getenv("PQD_QPW")) P->qpw = std::max(1, atoi(w));
+        if (P->quad) BT = 4;
+    }
     P->BT = BT;
     std::vector<int> bt, be, bs, ba, bsrc;
     {
@@ -856,6 +872,8 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     }
     sp.F = P->F.p; sp.W = P->W.p;
     sp.woff = P->woff.p; sp.ev_start = P->ev_start.p; sp.ev = P->ev.p; sp.sop = P->sop.p; sp.out = P->out.p;
+    sp.n_steps = ns;
+    sp.n_blk = nb;
     finalize_trunks(P);
     if (P->split) {
         HIPCHK(P->Xs.alloc((size_t)P->n_traj * 2 * N2 * P->CHI));
@@ -894,7 +912,7 @@ int pqd_plan_execute(pqd_plan* P, int32_t rebuild_free) {
     else if (P->split)
         HIPCHK(launch_split(P->N2, P->CHI, P->n_traj, P->sp, P->Xs.p, P->cnt.p, P->err.p, s));
     else
-        HIPCHK(launch_sweep(P->N2, P->CHI, P->BT, P->n_blocks, P->sp, s));
+        HIPCHK(launch_main(P, s));
     HIPCHK(hipEventRecord(e[2], s));
     P->ev_head = (P->ev_head + 1) % pqd_plan::RING;
     P->ev_count++;
@@ -922,7 +940,7 @@ int pqd_plan_synchronize(pqd_plan* P) {
             P->split_fallbacks++;
             HIPCHK(hipMemsetAsync(P->tk_err.p, 0, sizeof(unsigned), s));
             HIPCHK(launch_trunks(P, s));
-            HIPCHK(launch_sweep(P->N2, P->CHI, P->BT, P->n_blocks, P->sp, s));
+            HIPCHK(launch_main(P, s));
         }
     }
     if (P->split) {
@@ -933,7 +951,7 @@ int pqd_plan_synchronize(pqd_plan* P) {
             P->split = false;
             P->split_fallbacks++;
             HIPCHK(hipMemsetAsync(P->err.p, 0, sizeof(unsigned), s));
-            HIPCHK(launch_sweep(P->N2, P->CHI, P->BT, P->n_blocks, P->sp, s));
+            HIPCHK(launch_main(P, s));
         }
     }
     unsigned flags = 0;
@@ -959,7 +977,7 @@ int pqd_plan_download(pqd_plan* P, pqd_c128* out, int64_t out_len) {
 int pqd_plan_info(const pqd_plan* P, int32_t* path, int32_t* bt, int32_t* split_fallbacks, int64_t* traj_steps) {
     if (!P) return fail(PQD_ERR_ARG, "plan is NULL");
     if (traj_steps) *traj_steps = P->traj_steps;
-    if (path) *path = P->nopt ? PQD_PATH_NOPT : P->split ? PQD_PATH_SPLIT : PQD_PATH_BATCHED;
+    if (path) *path = P->nopt ? PQD_PATH_NOPT : P->split ? PQD_PATH_SPLIT : P->quad ? PQD_PATH_QUAD : PQD_PATH_BATCHED;
     if (bt) *bt = P->BT;
     if (split_fallbacks) *split_fallbacks = P->split_fallbacks;
     return PQD_OK;

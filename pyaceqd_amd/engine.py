@@ -293,7 +293,8 @@ class Plan:
         _lib.NumericError on NaN/Inf outputs"""
         _lib.check(_lib.lib().pqd_plan_synchronize(self.handle))
 
-    PATHS = {0: "no PT (one wave per trajectory)", 1: "batched lock-step sweep", 2: "split groups"}
+    PATHS = {0: "no PT (one wave per trajectory)", 1: "batched lock-step sweep", 2: "split groups",
+             3: "register-resident TLS quads"}
 
     def info(self):
         """(path name, trajectories per workgroup, split launches that fell back to the batched kernel)"""
