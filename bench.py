@@ -30,15 +30,15 @@ PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 (vector == matrix on gfx950), spec
 PEAK_HBM_GBS = 8000.0
 
 
-def build_workload(n_t1, n_tau, chi, scan=1, scan_offset=0, dt=0.1, seed=1234, dictionary=False):
-    """(systems, grid, pt, rho0, ops, traj): `scan` pulse-area points x `n_t1` t1 points"""
+def build_workload(n_t1, n_tau, chi, scan=1, scan_offset=0, dt=0.1, seed=1234, dictionary=False, t1_offset=0):
+    """(systems, grid, pt, rho0, ops, traj): `scan` pulse-area points x `n_t1` t1 points (t1 steps t1_offset ...)"""
     from pyaceqd_amd import engine, opgrammar, pt as ptmod
     from pyaceqd_amd.constants import hbar
     from pyaceqd_amd.four_level_system.linear import biexciton_ops
     from pyaceqd_amd.pulses import ChirpedPulse, PulseTrain
     N = 4
     so, bo, lo, io, _ = biexciton_ops(delta_b=4, lindblad=True)
-    t1_steps = np.arange(n_t1)
+    t1_steps = t1_offset + np.arange(n_t1)
     n_steps = int(t1_steps[-1] + n_tau)
     ds = dt / 4
     ts = ds * np.arange(4 * n_steps + 1)
@@ -190,6 +190,10 @@ def main():
     ap.add_argument("--chi", type=int, default=64)
     ap.add_argument("--pt-dict", type=int, default=0,
                     help="1: dictionary PT (9 slices for the 16 rows, as generated physical PTs have); 0: 16 slices")
+    ap.add_argument("--shard", choices=["scan", "t1"], default="scan",
+                    help="multi-GPU partition (SURVEY.md §8e): scan = rank r runs scan points [r*scan, (r+1)*scan) with "
+                         "the whole t1 grid; t1 = every rank runs the same scan points and its block of a t1 grid of "
+                         "t1*world points")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
@@ -201,7 +205,8 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as dist
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # nccl (= RCCL over xGMI) on the GPU node; PQD_DIST_BACKEND=gloo rehearses the multi-rank path on one GPU
+        backend = os.environ.get("PQD_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
@@ -209,14 +214,20 @@ def main():
 
     from pyaceqd_amd import _lib, engine
     ctx = _lib.context(local)
-    sysd, grid, pt, rho0, ops, tr = build_workload(args.t1, args.n_tau, args.chi, scan=args.scan,
-                                                   scan_offset=rank * args.scan, dictionary=bool(args.pt_dict))
+    from pyaceqd_amd import scan as scanmod
+    if args.shard == "t1":
+        t1_lo, t1_hi = scanmod.shard_range(args.t1 * world, rank, world)
+        sysd, grid, pt, rho0, ops, tr = build_workload(t1_hi - t1_lo, args.n_tau, args.chi, scan=args.scan,
+                                                       dictionary=bool(args.pt_dict), t1_offset=t1_lo)
+    else:
+        sysd, grid, pt, rho0, ops, tr = build_workload(args.t1, args.n_tau, args.chi, scan=args.scan,
+                                                       scan_offset=rank * args.scan, dictionary=bool(args.pt_dict))
     n_traj = tr.n_traj
     plan = engine.Plan(sysd, grid, rho0, ops, tr, pt=pt, ctx=ctx)
 
     def barrier():
         if dist is not None:
-            if torch.cuda.is_available():
+            if torch.cuda.is_available() and dist.get_backend() == "nccl":
                 dist.barrier(device_ids=[local])
             else:
                 dist.barrier()
@@ -239,14 +250,24 @@ def main():
     ms_free, ms_sweep, nexec = plan.timing(reset=True)
     if dist is not None:
         t = torch.tensor([el, ms_sweep, ms_free], dtype=torch.float64,
-                         device=f"cuda:{local}" if torch.cuda.is_available() else "cpu")
+                         device=f"cuda:{local}" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, ms_sweep, ms_free = [float(x) for x in t.tolist()]
 
-    # sanity on the last result (outside the timed region): trace-free check of <B> bounds
-    res = plan.download()
-    g0 = np.array([r[0, 1] for r in res])
-    assert np.all(np.isfinite(g0)), "non-finite output"
+    # the one collective (outside the timed region): every rank's output block gathered in rank order through a
+    # device-buffer all_gather (RCCL over xGMI; scan.gather_tensor); then a finite check of the whole result
+    t0g = time.perf_counter()
+    on_host = dist is not None and dist.get_backend() == "gloo"  # gloo gathers host tensors
+    local_out = plan.output_tensor(device="cpu" if on_host else None)
+    allout = scanmod.gather_tensor(local_out, dist)
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    gather_ms = (time.perf_counter() - t0g) * 1e3
+    assert bool(torch.isfinite(torch.view_as_real(allout)).all()), "non-finite output"
+    gather = {"collective": "all_gather_into_tensor" if dist is not None else "none (one rank)",
+              "backend": (dist.get_backend() if dist is not None else None), "values": int(allout.numel()),
+              "bytes": int(allout.numel()) * 16, "ms": gather_ms,
+              "checksum": float(torch.view_as_real(allout).abs().sum())}
 
     useful = n_traj * args.n_tau
     executed = plan.traj_steps()   # shared trunks (PQD_BRANCH) counted once per workgroup
@@ -276,7 +297,8 @@ def main():
                    "traj_per_gpu": n_traj, "scan_points_per_gpu": args.scan, "t1_points": args.t1,
                    "grid_steps": grid.n_steps,
                    "useful_traj_steps_per_gpu": useful, "executed_traj_steps_per_gpu": executed,
-                   "parallelism": f"scan{world}", "kernel_ms": {"pt_sweep": ms_sweep, "free_prop": ms_free}},
+                   "parallelism": f"{args.shard}{world}", "kernel_ms": {"pt_sweep": ms_sweep, "free_prop": ms_free},
+                   "gather": gather},
         "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tf / PEAK_FP64_TFLOPS, "traffic": traffic,
                      "traffic_unit": "HBM bytes per launch", "traffic_source": traffic_src,

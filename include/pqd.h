@@ -146,6 +146,10 @@ void* pqd_plan_output_device(pqd_plan* plan);
 int pqd_plan_synchronize(pqd_plan* plan);
 /* pqd_plan_synchronize + copy of the outputs (also on PQD_ERR_NUMERIC, which is still returned) */
 int pqd_plan_download(pqd_plan* plan, pqd_c128* out, int64_t out_len);
+/* pqd_plan_synchronize + copy of the outputs into `dst`, a device buffer of the plan's device (or host memory) of
+ * out_len complex values, e.g. a torch tensor that a collective then gathers over xGMI (scan.py). Replaces the
+ * reference's result lists assembled from per-process CSV files (correlations.py:171-183). */
+int pqd_plan_copy_output(pqd_plan* plan, void* dst, int64_t out_len);
 #define PQD_PATH_NOPT 0     /* no PT: one wave per trajectory */
 #define PQD_PATH_BATCHED 1  /* lock-step PT sweep, bt trajectories per workgroup */
 #define PQD_PATH_SPLIT 2    /* one trajectory over N^2 workgroups (latency path) */

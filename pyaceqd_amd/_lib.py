@@ -78,6 +78,7 @@ _SIGS = {
     "pqd_plan_output_device": ([C.c_void_p], C.c_void_p),
     "pqd_plan_synchronize": ([C.c_void_p], C.c_int),
     "pqd_plan_download": ([C.c_void_p, P_C128, C.c_int64], C.c_int),
+    "pqd_plan_copy_output": ([C.c_void_p, C.c_void_p, C.c_int64], C.c_int),
     "pqd_plan_info": ([C.c_void_p, P_I32, P_I32, P_I32, P_I64], C.c_int),
     "pqd_plan_timing": ([C.c_void_p, P_F64, P_F64, P_I32, C.c_int32], C.c_int),
     "pqd_plan_destroy": ([C.c_void_p], None),

@@ -974,6 +974,18 @@ int pqd_plan_download(pqd_plan* P, pqd_c128* out, int64_t out_len) {
     return rc;  // PQD_ERR_NUMERIC still hands the values over (they show where the run went bad)
 }
 
+int pqd_plan_copy_output(pqd_plan* P, void* dst, int64_t out_len) {
+    if (!P || !dst) return fail(PQD_ERR_ARG, "NULL argument");
+    if (out_len < P->out_len) return fail(PQD_ERR_ARG, "out_len %lld < plan out_len %lld", (long long)out_len, (long long)P->out_len);
+    int rc = pqd_plan_synchronize(P);
+    if (rc && rc != PQD_ERR_NUMERIC) return rc;
+    if (P->out_len > 0) {
+        HIPCHK(hipMemcpyAsync(dst, P->out.p, P->out_len * sizeof(double2), hipMemcpyDefault, P->ctx->stream));
+        HIPCHK(hipStreamSynchronize(P->ctx->stream));
+    }
+    return rc;
+}
+
 int pqd_plan_info(const pqd_plan* P, int32_t* path, int32_t* bt, int32_t* split_fallbacks, int64_t* traj_steps) {
     if (!P) return fail(PQD_ERR_ARG, "plan is NULL");
     if (traj_steps) *traj_steps = P->traj_steps;

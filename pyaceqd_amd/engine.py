@@ -311,6 +311,15 @@ class Plan:
     def output_device_ptr(self):
         return _lib.lib().pqd_plan_output_device(self.handle)
 
+    def output_tensor(self, device=None):
+        """the outputs as one flat complex128 torch tensor on `device` (default: this plan's GPU), copied device to
+        device after synchronize; the input of a collective gather (scan.gather_tensor)"""
+        import torch
+        dev = torch.device(device) if device is not None else torch.device("cuda", self.ctx.device)
+        t = torch.empty(max(1, self.total), dtype=torch.complex128, device=dev)
+        _lib.check(_lib.lib().pqd_plan_copy_output(self.handle, C.c_void_p(t.data_ptr()), max(1, self.total)))
+        return t[: self.total]
+
     def download(self):
         out = np.zeros(max(1, self.total), dtype=np.complex128)
         _lib.check(_lib.lib().pqd_plan_download(self.handle, _lib.cptr(out), max(1, self.total)))

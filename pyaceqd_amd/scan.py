@@ -42,6 +42,32 @@ def gather_blocks(local, dist=None, dst=0):
     return out
 
 
+def gather_tensor(local, dist=None):
+    """Every rank's 1-D tensor (any length, any device) concatenated in rank order, on every rank.
+
+    One all_gather of the block lengths, then one all_gather_into_tensor of the blocks padded to the longest, on the
+    tensors' own device: RCCL over xGMI for GPU tensors (the result blocks never pass through host memory), gloo for
+    CPU tensors. Complex blocks travel as their real view. This is the one collective of a sharded sweep (SURVEY.md
+    §8e); the reference assembles its result lists from per-process CSV files (correlations.py:171-183)."""
+    import torch
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return local
+    world = dist.get_world_size()
+    cplx = local.is_complex()
+    x = (torch.view_as_real(local) if cplx else local).reshape(-1).contiguous()
+    n = torch.tensor([x.numel()], dtype=torch.int64, device=x.device)
+    ns = torch.empty(world, dtype=torch.int64, device=x.device)
+    dist.all_gather_into_tensor(ns, n)
+    sizes = [int(v) for v in ns.tolist()]
+    m = max(sizes)
+    buf = torch.zeros(max(1, m), dtype=x.dtype, device=x.device)
+    buf[: x.numel()] = x
+    out = torch.empty(world * max(1, m), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, buf)
+    y = torch.cat([out[r * max(1, m): r * max(1, m) + sizes[r]] for r in range(world)])
+    return torch.view_as_complex(y.reshape(-1, 2)) if cplx else y
+
+
 def run_sharded(units, work, dist=None):
     """Run `work(block_of_units) -> list of results` on this rank's block and gather to rank 0."""
     if dist is not None and dist.is_initialized():

@@ -1,6 +1,10 @@
-"""Multi-rank path on CPU (gloo, world_size 2): a pulse-area scan sharded over ranks, each rank
-propagating its block (through the CPU oracle here; on the GPU box the same code drives libpqd),
-gathered to rank 0 and compared with the single-process result."""
+"""Multi-rank paths (world_size 2, 127.0.0.1 rendezvous).
+
+CPU (gloo): a pulse-area scan sharded over ranks through the CPU oracle and gathered to rank 0; the device-buffer
+gather (scan.gather_tensor: all_gather_into_tensor of ragged complex blocks) against a local concatenation.
+GPU (gloo, two processes on the one GPU of the box): the bench's two-time sweep with its t1 grid sharded over the
+ranks (bench.py --shard t1), each rank propagating its block through libpqd (the batched kernel),
+gathered with scan.gather_tensor and compared bit for bit with one process propagating the whole grid."""
 import os
 import socket
 
@@ -9,7 +13,7 @@ import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from pyaceqd_amd.scan import gather_blocks, run_sharded, shard_range
+from pyaceqd_amd.scan import gather_blocks, gather_tensor, run_sharded, shard_range
 
 
 def test_shard_range_partitions():
@@ -71,3 +75,84 @@ def test_gloo_world2_scan_matches_single_process():
 
 def test_gather_blocks_single_process_passthrough():
     assert [int(x) for x in gather_blocks([np.array(1), np.array(2)], None)] == [1, 2]
+
+
+def _gather_worker(rank, world, port, q):
+    import torch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 3 + 4 * rank  # ragged blocks
+    x = torch.arange(n, dtype=torch.float64) * (1 + 1j) + 100 * rank
+    y = gather_tensor(x.to(torch.complex128), dist)
+    q.put((rank, y.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_tensor_ragged_complex_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    ref = np.concatenate([np.arange(3 + 4 * r) * (1 + 1j) + 100 * r for r in range(2)])
+    for r in range(2):
+        assert np.array_equal(got[r], ref)
+
+
+N_T1, N_TAU, CHI = 16, 60, 16
+
+
+def _t1_block_worker(rank, world, port, q):
+    try:
+        import bench
+        from pyaceqd_amd import _lib, engine, scan
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        lo, hi = scan.shard_range(N_T1, rank, world)
+        sysd, grid, pt, rho0, ops, tr = bench.build_workload(hi - lo, N_TAU, CHI, t1_offset=lo)
+        plan = engine.Plan(sysd, grid, rho0, ops, tr, pt=pt, ctx=_lib.context(0))
+        plan.execute()
+        path = plan.info()[0]
+        y = gather_tensor(plan.output_tensor(device="cpu"), dist)
+        if rank == 0:
+            q.put(("ok", path, y.numpy()))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of leaving the peer in its collective
+        q.put(("err", rank, repr(e)))
+        raise
+
+
+@pytest.mark.gpu
+def test_gloo_world2_t1_sharded_sweep_matches_single_process(monkeypatch):
+    monkeypatch.setenv("PQD_SPLIT", "0")  # the batched kernel on both ranks and in the single process
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_t1_block_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    msg = q.get(timeout=100)
+    if msg[0] != "ok":
+        for p in procs:
+            p.kill()
+        pytest.fail(f"rank {msg[1]}: {msg[2]}")
+    _, path, got = msg
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert path == "batched lock-step sweep"
+    import bench
+    from pyaceqd_amd import engine
+    sysd, grid, pt, rho0, ops, tr = bench.build_workload(N_T1, N_TAU, CHI)
+    plan = engine.Plan(sysd, grid, rho0, ops, tr, pt=pt)
+    plan.execute()
+    ref = np.concatenate([r.ravel() for r in plan.download()])
+    assert got.shape == ref.shape
+    assert np.array_equal(got, ref)
