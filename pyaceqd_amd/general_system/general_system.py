@@ -169,8 +169,9 @@ def system_ace_stream(t_start, t_end, *pulses, dt=0.01, phonons=False, t_mem=20.
     Returns (1 + len(output_ops), n_t) complex, row 0 = time (general_system.py:104-110, 343).
     With calc_dynmap: (result, dm) with dm[i] = E(t_{i+1}, t_start) acting on row-major vec(rho)
     (general_system.py:313-336, 358-359). With `trajectories` (list of dicts with keys "multitime_op", "t_end",
-    optionally "out_begin" and a per-trajectory drive "pulses" / "pulse_file_x" / "pulse_file_y"): a list of
-    per-trajectory results, all propagated in one launch (one System per distinct drive: parameter scans).
+    optionally "out_begin", a per-trajectory drive "pulses" / "pulse_file_x" / "pulse_file_y" and per-trajectory
+    "system_op" / "lindblad_ops" replacing the call's): a list of per-trajectory results, all propagated in one launch
+    (one System per distinct drive and generator: parameter scans over pulses and fields).
     """
     sanity_checks(system_op, phonons, boson_op, initial, interaction_ops, verbose)
     if multitime_op is not None:
@@ -198,10 +199,14 @@ def system_ace_stream(t_start, t_end, *pulses, dt=0.01, phonons=False, t_mem=20.
     if dim is None:
         dim = 2  # "assuming TLS" (:19)
     mat = lambda s: opgrammar.to_matrix(s, dim)  # noqa: E731
-    H0 = np.zeros((dim, dim), dtype=complex)
-    for s in (system_op or []):
-        H0 = H0 + mat(s)
-    lind = [(float(rate), mat(op)) for op, rate in (lindblad_ops or [])]
+    def hamiltonian(ops):
+        H = np.zeros((dim, dim), dtype=complex)
+        for s in (ops or []):
+            H = H + mat(s)
+        return H
+
+    def dissipators(ops):
+        return [(float(rate), mat(op)) for op, rate in (ops or [])]
     rho_init = mat(initial) if initial is not None else np.diag([1.0] + [0.0] * (dim - 1)).astype(complex)
     if rho0 is not None:
         rho_init = np.asarray(rho0, dtype=complex).reshape(dim, dim)
@@ -225,7 +230,7 @@ def system_ace_stream(t_start, t_end, *pulses, dt=0.01, phonons=False, t_mem=20.
     ds = dt / (4 * n_sub)
     ts = t_start + ds * np.arange(4 * n_sub * n_steps + 1)
 
-    def make_system(pulse_list, pfx, pfy):
+    def make_system(pulse_list, pfx, pfy, H0, lind):
         channels, t0s, dts = [], [], []
         use_pulses = [pulse_list[0]] if (firstonly and pulse_list) else list(pulse_list)
         if rf_op is not None and rf_file is None:
@@ -279,10 +284,12 @@ def system_ace_stream(t_start, t_end, *pulses, dt=0.01, phonons=False, t_mem=20.
         pl = tuple(spec["pulses"]) if "pulses" in spec else tuple(pulses)
         pfx = spec.get("pulse_file_x", pulse_file_x)
         pfy = spec.get("pulse_file_y", pulse_file_y)
-        key = (tuple(id(p) for p in pl), pfx, pfy)
+        sop = spec.get("system_op", system_op)
+        lop = spec.get("lindblad_ops", lindblad_ops)
+        key = (tuple(id(p) for p in pl), pfx, pfy, tuple(sop or ()), tuple((str(o), float(r)) for o, r in (lop or ())))
         if key not in sys_keys:
             sys_keys[key] = len(systems)
-            systems.append(make_system(pl, pfx, pfy))
+            systems.append(make_system(pl, pfx, pfy, hamiltonian(sop), dissipators(lop)))
         traj_sys.append(sys_keys[key])
     system = systems[0]
 

@@ -109,18 +109,38 @@ class PolarizatzionEntanglement():
         opts["output_ops"] = output_ops
         return self.system(0, t_end_max, trajectories=specs, **opts)
 
-    def _g2_runs(self, op1_t, op23s, op4_t):
-        """one trajectory per t1: op4 from the left and op1 from the right at t1, outputs <op2 op3> for every pair
-        and <op1 op2 op3 op4>; returns per-t1 arrays (1 + 2 n_pairs, n_t2 + 1) starting at step int(t1/dt)"""
+    def _g2_specs(self, op1_t, op23s, op4_t):
+        """one trajectory per t1 (reference :467-482): op4 from the left and op1 from the right at t1, every
+        trajectory to tend, its outputs from step int(t1/dt) on; output operators <op2 op3> for every pair, then
+        <op1 op2 op3 op4>"""
         tau0 = [op1_t + " * " + o + " * " + op4_t for o in op23s]
-        n_tau = int(self.tend / self.dt)
-        begins = [max(0, int(t / self.dt)) for t in self.t1]
+        specs = [{"multitime_op": [{"operator": op1_t, "applyFrom": "_right", "applyBefore": "false", "time": t},
+                                   {"operator": op4_t, "applyFrom": "_left", "applyBefore": "false", "time": t}],
+                  "t_end": self.tend, "out_begin": max(0, int(t / self.dt))} for t in self.t1]
+        return specs, list(op23s) + tau0, int(self.tend / self.dt)
 
-        def mt(i):
-            return [{"operator": op1_t, "applyFrom": "_right", "applyBefore": "false", "time": self.t1[i]},
-                    {"operator": op4_t, "applyFrom": "_left", "applyBefore": "false", "time": self.t1[i]}]
-        res = self._batch(lambda i: self.tend, lambda i: begins[i], mt, list(op23s) + tau0, self.tend)
-        return n_tau, res
+    def _g2_runs(self, op1_t, op23s, op4_t):
+        """per-t1 arrays (1 + 2 n_pairs, n_t2 + 1) starting at step int(t1/dt), one launch"""
+        specs, outs, n_tau = self._g2_specs(op1_t, op23s, op4_t)
+        opts = dict(self.options)
+        opts["output_ops"] = outs
+        return n_tau, self.system(0, self.tend, trajectories=specs, **opts)
+
+    def _reuse_integrals(self, res, n_pairs, n_tau, return_full_G2=False):
+        """tau and t1 integrals of G2_reuse from the per-t1 rows (reference :484-505)"""
+        t1 = self.t1
+        t2 = np.linspace(0, self.tend, n_tau + 1)
+        g = np.zeros((n_pairs, len(t1)), dtype=complex)
+        full = np.zeros((n_pairs, len(t1), n_tau + 1), dtype=complex) if return_full_G2 else None
+        for i, r in enumerate(res):
+            n_t2 = n_tau - int(t1[i] / self.dt)
+            rows = self._g2_rows(r, n_pairs, n_t2)
+            if return_full_G2:
+                full[:, i, : n_t2 + 1] = rows
+            g[:, i] = _trapz(rows, t2[: n_t2 + 1], axis=1)
+        if return_full_G2:
+            return t1, t2, g, _trapz(g, t1, axis=1), full
+        return t1, g, _trapz(g, t1, axis=1)
 
     @staticmethod
     def _g2_rows(r, n_pairs, n_t2):
@@ -198,21 +218,8 @@ class PolarizatzionEntanglement():
 
     def G2_reuse(self, op1_t, op23s_ttau, op4_t, return_full_G2=False):
         """G2 for several (op2 op3) pairs from one propagation per t1 (reference :423-505)"""
-        n_pairs = len(op23s_ttau)
         n_tau, res = self._g2_runs(op1_t, list(op23s_ttau), op4_t)
-        t1 = self.t1
-        t2 = np.linspace(0, self.tend, n_tau + 1)
-        g = np.zeros((n_pairs, len(t1)), dtype=complex)
-        full = np.zeros((n_pairs, len(t1), n_tau + 1), dtype=complex) if return_full_G2 else None
-        for i, r in enumerate(res):
-            n_t2 = n_tau - int(t1[i] / self.dt)
-            rows = self._g2_rows(r, n_pairs, n_t2)
-            if return_full_G2:
-                full[:, i, : n_t2 + 1] = rows
-            g[:, i] = _trapz(rows, t2[: n_t2 + 1], axis=1)
-        if return_full_G2:
-            return t1, t2, g, _trapz(g, t1, axis=1), full
-        return t1, g, _trapz(g, t1, axis=1)
+        return self._reuse_integrals(res, len(op23s_ttau), n_tau, return_full_G2)
 
     # ------------------------------------------------------------------ two-photon density matrix
     def _pairs_x(self):
@@ -246,11 +253,14 @@ class PolarizatzionEntanglement():
         rho = self._assemble(np.array(v, dtype=complex)[:, None], abs_diag=False)[0]
         return concurrence(rho / np.trace(rho))
 
-    def calc_densitymatrix_reuse(self, plot_G2=None, return_counts=False, return_rho=False):
-        """three G2_reuse runs (op1, op4) = (x, x), (x, y), (y, y) (reference :299-354)"""
-        t1, G1t, G1 = self.G2_reuse(self.axdag, self._pairs_x(), self.ax)
-        t2, G2t, G2 = self.G2_reuse(self.axdag, self._pairs_xy(), self.ay)
-        t3, G3t, G3 = self.G2_reuse(self.aydag, self._pairs_x(), self.ay)
+    def _reuse_variants(self):
+        """the three G2_reuse runs of calc_densitymatrix_reuse: (op1, op23s, op4) = (x, x), (x, y), (y, y)"""
+        return [(self.axdag, self._pairs_x(), self.ax), (self.axdag, self._pairs_xy(), self.ay),
+                (self.aydag, self._pairs_x(), self.ay)]
+
+    def _densitymatrix_from(self, G, plot_G2=None, return_counts=False, return_rho=False):
+        """reference :313-354 from the three G2_reuse results G = [(t1, G_t, G_int)] * 3"""
+        (t1, G1t, G1), (t2, G2t, G2), (t3, G3t, G3) = G
         v = np.array([G1[0], G1[1], G1[2], G2[0], G2[1], G2[2], G2[3], G3[0], G3[1], G3[2]])
         rho = self._assemble(v[:, None])[0]
         norm = np.trace(rho)
@@ -262,6 +272,11 @@ class PolarizatzionEntanglement():
         if return_counts:
             return concurrence(rho / norm), rho[0, 0], rho[1, 1], rho[2, 2], rho[3, 3], rho[0, 3]
         return concurrence(rho / norm)
+
+    def calc_densitymatrix_reuse(self, plot_G2=None, return_counts=False, return_rho=False):
+        """three G2_reuse runs (op1, op4) = (x, x), (x, y), (y, y) (reference :299-354)"""
+        G = [self.G2_reuse(*v) for v in self._reuse_variants()]
+        return self._densitymatrix_from(G, plot_G2, return_counts, return_rho)
 
     def calc_timedep_data(self):
         """full G2(t, tau) of the 10 components (reference :357-371)"""
@@ -313,3 +328,41 @@ class PolarizatzionEntanglement():
             inner = np.where(m > 0, cum[:, np.arange(i + 1), np.maximum(m - 1, 0)], 0.0)
             G2_t[:, i] = _trapz(inner, t1[: i + 1], axis=1)
         return t1, G2_t
+
+
+def densitymatrix_reuse_scan(instances, model_kwargs=None, return_rho=False):
+    """`calc_densitymatrix_reuse` for every point of a pulse / field scan in three launches in total.
+
+    The reference runs each point on its own (one `PolarizatzionEntanglement` per point, ACE processes per t1 and
+    G2_reuse: pol_entanglement/G2.py:299-354, 467-482). Here the instances (one per scan point, each with its own
+    pulses / pulse files and t1 grid) share their model callable, dt and tend; `model_kwargs[i]` (e.g. {"bx": 2.0})
+    are per-point model keywords the model turns into per-trajectory generators (six_level_system.linear). Each of
+    the three G2_reuse variants becomes ONE launch holding every point's t1 trajectories.
+    Returns the list of concurrences (with return_rho, (concurrence, rho) pairs), in the order of `instances`."""
+    insts = list(instances)
+    if not insts:
+        return []
+    kw = list(model_kwargs) if model_kwargs is not None else [{}] * len(insts)
+    first = insts[0]
+    for x in insts[1:]:
+        if x.dt != first.dt or x.tend != first.tend:
+            raise ValueError("the points of a scan must share dt and tend")
+    per = [[] for _ in insts]
+    for v in range(3):
+        specs, counts, outs, n_tau = [], [], None, None
+        for x, k in zip(insts, kw):
+            sp, outs, n_tau = x._g2_specs(*x._reuse_variants()[v])
+            for spec in sp:
+                spec["pulse_file_x"] = x.options.get("pulse_file_x")
+                spec["pulse_file_y"] = x.options.get("pulse_file_y")
+                spec.update(k)
+            specs += sp
+            counts.append(len(sp))
+        opts = dict(first.options)
+        opts["output_ops"] = outs
+        res = first.system(0, first.tend, trajectories=specs, **opts)
+        o = 0
+        for i, x in enumerate(insts):
+            per[i].append(x._reuse_integrals(res[o: o + counts[i]], len(x._reuse_variants()[v][1]), n_tau))
+            o += counts[i]
+    return [x._densitymatrix_from(G, return_rho=return_rho) for x, G in zip(insts, per)]

@@ -69,6 +69,17 @@ def sixls_linear(t_start, t_end, *pulses, dt=0.5, delta_b=4, gamma_e=1/100, gamm
     if output_dm:
         output_ops = output_ops_dm(dim=6)
     fwd = {k: options[k] for k in _FWD if k in options}
+    if fwd.get("trajectories") is not None:
+        # per-trajectory magnetic fields (an e0 x bx scan in one launch): a spec's "bx" / "bz" become its own
+        # system_op, the strings this function writes for those fields
+        specs = []
+        for spec in fwd["trajectories"]:
+            if "bx" in spec or "bz" in spec:
+                spec = dict(spec)
+                spec["system_op"] = sixls_ops(delta_b, gamma_e, gamma_b, gamma_d, spec.pop("bx", bx),
+                                              spec.pop("bz", bz), lindblad, rf, d0, d1, d2)[0]
+            specs.append(spec)
+        fwd["trajectories"] = specs
     result = system_ace_stream(
         t_start, t_end, *pulses, dt=dt, phonons=phonons, t_mem=t_mem, ae=ae, temperature=temperature,
         verbose=verbose, temp_dir=temp_dir, pt_file=pt_file, suffix=suffix, multitime_op=multitime_op,

@@ -10,6 +10,9 @@ algorithmic flops (fused half steps: F = 8 (D chi^2 + chi N^4 + n_out N^2), D = 
   c5      six-level linear model, N=6, chi=64, 32 scan points x 64 t1 points = 2048 trajectories, 2,000 tau steps
   c5d     c5 with a dictionary PT (9 slices for the 36 rows, as a generated physical PT has)
   c3d     the bench workload at n_tau = 2,000 with a dictionary PT (9 slices for the 16 rows)
+  c5dm    C5 as specified: sixls_linear + polarisation-entanglement tomography (calc_densitymatrix_reuse) over an
+          e0 x bx grid (2 x {0, 1, 2, 4} points, tests/six_level_linear.py pulse pair, tend 400 ps, dt 0.1 ps, the
+          class's t1 grid, chi = 64 dictionary PT), three launches for the whole grid (densitymatrix_reuse_scan)
 usage: python scripts/bench_configs.py [--configs c1,c2,c3one,c5] [--steps 3]
 """
 import argparse
@@ -134,13 +137,48 @@ def run(name, steps):
             "traj_steps_per_s": executed / el, "flop_per_traj_step": F, "sweep_TFLOPs": tf, "frac_fp64": tf / PEAK}
 
 
+def run_c5dm(steps, n_e0=2, bxs=(0.0, 1.0, 2.0, 4.0), tend=400.0):
+    import tempfile
+    from pyaceqd_amd import opgrammar, pt as ptmod
+    from pyaceqd_amd.pol_entanglement.G2 import PolarizatzionEntanglement, densitymatrix_reuse_scan
+    from pyaceqd_amd.pulses import ChirpedPulse
+    from pyaceqd_amd.six_level_system.linear import energies_linear, sixls_linear, sixls_ops
+    E_X, _, _, _, E_B = energies_linear(delta_B=4)
+    pt = ptmod.synthetic_pt(opgrammar.to_matrix(sixls_ops()[1], 6), chi=64, n_init=410, n_rep=1, seed=1234,
+                            eps=0.05, dt=0.1, dictionary=True)
+    tmp = tempfile.mkdtemp() + "/"
+    insts, kws = [], []
+    for e0 in np.linspace(1, 10, 64)[:: 64 // n_e0][:n_e0]:
+        for bx in bxs:
+            p1 = ChirpedPulse(tau_0=2.7, e_start=E_X, alpha=40, e0=e0)
+            p2 = ChirpedPulse(tau_0=2.7, e_start=E_B - E_X, alpha=40, e0=4.06, t0=120)
+            opts = {"lindblad": True, "gamma_e": 1 / 100, "phonons": True, "pt_file": pt, "temp_dir": tmp}
+            insts.append(PolarizatzionEntanglement(sixls_linear, "|0><1|_6 + |1><5|_6", "|0><2|_6 + |2><5|_6",
+                                                   "|1><0|_6 + |5><1|_6", "|2><0|_6 + |5><2|_6", p1, p2, dt=0.1,
+                                                   tend=tend, options=opts))
+            kws.append({"bx": bx})
+    densitymatrix_reuse_scan(insts, kws)  # warm-up (PT upload, kernels)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        conc = densitymatrix_reuse_scan(insts, kws)
+    el = (time.perf_counter() - t0) / steps
+    n_traj = 3 * sum(len(x.t1) for x in insts)
+    n_tau = int(round(tend / 0.1))
+    executed = 3 * sum(int(np.sum(n_tau + 1 - np.minimum(n_tau, (np.asarray(x.t1) / 0.1).astype(int))))
+                       for x in insts)
+    return {"config": "c5dm", "model": "sixls", "points": len(insts), "e0": n_e0, "bx": list(bxs), "tend": tend,
+            "chi": 64, "N": 6, "n_out": "6/8/6", "launches": 3, "n_traj": n_traj,
+            "output_traj_steps": executed, "wall_s_per_scan": el, "points_per_s": len(insts) / el,
+            "output_traj_steps_per_s": executed / el, "concurrence": [float(c) for c in conc]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="c1,c2,c3one,c5")
     ap.add_argument("--steps", type=int, default=3)
     args = ap.parse_args()
     for name in args.configs.split(","):
-        print(json.dumps(run(name, args.steps)), flush=True)
+        print(json.dumps(run_c5dm(args.steps) if name == "c5dm" else run(name, args.steps)), flush=True)
 
 
 if __name__ == "__main__":
