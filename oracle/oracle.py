@@ -12,7 +12,7 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(_HERE, "liboracle.so")
+LIB = os.environ.get("PQD_ORACLE_LIB") or os.path.join(_HERE, "liboracle.so")  # tests/test_asan.py: ASan build
 _lib = None
 
 P_C = C.POINTER(C.c_double)  # complex as interleaved doubles

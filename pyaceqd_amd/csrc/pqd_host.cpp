@@ -763,7 +763,11 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     if (const char* e = getenv("PQD_TRUNK")) trunk_mode = atoi(e);
     bool use_trunk = false;
     if (branch_on && fuse_on && trunk_mode != 0 && ns > 0) {
-        int64_t crit_no = 0, crit_tk = 0, max_ck = 0;
+        // estimated main-sweep time in steps of one block: the longest block (critical path) or, with more blocks than
+        // the device holds at once, the total block-steps over the resident blocks, whichever is larger. Without the
+        // pre-pass a block spans [0, end] (its chain's first slot carries the trunk from step 0, dormant slots cost a
+        // lock-step block the same), with it [first activation, end]
+        int64_t crit_no = 0, crit_tk = 0, max_ck = 0, sum_no = 0, sum_tk = 0;
         const int nbk = (int)be.size();
         for (int b = 0; b < nbk; ++b) {
             int start = INT_MAX;
@@ -776,12 +780,26 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
                 if (a >= 1) { ck_steps[tsys[t]].push_back(a); max_ck = std::max<int64_t>(max_ck, a); }
             }
             crit_no = std::max<int64_t>(crit_no, be[b]);
-            if (start != INT_MAX) crit_tk = std::max<int64_t>(crit_tk, be[b] - start);
+            sum_no += be[b];
+            if (start != INT_MAX) {
+                crit_tk = std::max<int64_t>(crit_tk, be[b] - start);
+                sum_tk += be[b] - start;
+            }
         }
+        // blocks resident at once: quads (one workgroup of qpw quads per CU) or BT-workgroups as the LDS allows
+        int64_t conc = n_cu;
+        if (P->quad) {
+            conc = (int64_t)n_cu * std::max(1, P->qpw);
+        } else {
+            const int64_t lds = ((int64_t)BT * (N2 * (P->CHI + 1) + 4) + (int64_t)BT * N2) * 16;
+            conc = (int64_t)n_cu * std::max<int64_t>(1, std::min<int64_t>(4, (160 * 1024) / std::max<int64_t>(1, lds)));
+        }
+        const double t_no = std::max((double)crit_no, (double)sum_no / (double)conc);
+        const double t_tk = std::max((double)crit_tk, (double)sum_tk / (double)conc);
         // trunk step latency relative to a lock-step main-sweep step: split groups (N2 >= 9) ~0.5, one batched
         // workgroup ~0.7
         const double r = N2 >= 9 ? 0.5 : 0.7;
-        use_trunk = max_ck > 0 && (trunk_mode == 1 || (double)crit_tk + r * (double)max_ck < 0.995 * (double)crit_no);
+        use_trunk = max_ck > 0 && (trunk_mode == 1 || t_tk + r * (double)max_ck < 0.995 * t_no);
     }
     if (use_trunk) {
         std::vector<int> ck_base(n_sys, 0);

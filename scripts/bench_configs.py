@@ -10,6 +10,9 @@ algorithmic flops (fused half steps: F = 8 (D chi^2 + chi N^4 + n_out N^2), D = 
   c5      six-level linear model, N=6, chi=64, 32 scan points x 64 t1 points = 2048 trajectories, 2,000 tau steps
   c5d     c5 with a dictionary PT (9 slices for the 36 rows, as a generated physical PT has)
   c3d     the bench workload at n_tau = 2,000 with a dictionary PT (9 slices for the 16 rows)
+  c4reuse G2_reuse-shaped biexciton sweep (reference pol_entanglement/G2.py:486-497): 8 scan points x 1024 t1 points
+          spread over [0, tend), every trajectory from step 0 to tend = 4,096 steps with its MTOs at t1, chi = 64;
+          run without (PQD_BRANCH=0) and with shared trunks: executed vs useful traj-steps and wall per launch
   c5dm    C5 as specified: sixls_linear + polarisation-entanglement tomography (calc_densitymatrix_reuse) over an
           e0 x bx grid (2 x {0, 1, 2, 4} points, tests/six_level_linear.py pulse pair, tend 400 ps, dt 0.1 ps, the
           class's t1 grid, chi = 64 dictionary PT), three launches for the whole grid (densitymatrix_reuse_scan)
@@ -137,6 +140,50 @@ def run(name, steps):
             "traj_steps_per_s": executed / el, "flop_per_traj_step": F, "sweep_TFLOPs": tf, "frac_fp64": tf / PEAK}
 
 
+def run_c4reuse(steps, n_scan=8, n_t1=1024, n_steps=4096, chi=64):
+    import bench
+    from pyaceqd_amd import engine
+    systems, grid, pt, rho0, ops, tr = bench.build_workload(1, n_steps, chi, scan=n_scan)
+    # the same systems and PT on a G2_reuse grid: t1 = k * n_steps / n_t1, windows [t1, tend], MTOs at t1
+    A, Cm = [m.op for m in tr.mtos[:2]]
+    t1s = (np.arange(n_t1) * n_steps) // n_t1
+    mtos, beg, end, sysidx = [], [], [], []
+    for k in range(n_scan):
+        for t1 in t1s:
+            t = len(beg)
+            mtos += [engine.MTO(t, int(t1), False, 2, A), engine.MTO(t, int(t1), False, 1, Cm)]
+            beg.append(int(t1))
+            end.append(n_steps)
+            sysidx.append(k)
+    tr = engine.Trajectories(np.array(beg), np.array(end), mtos, system=np.array(sysidx))
+    grid = engine.Grid(0.0, grid.dt, n_steps, 1)
+    useful = int(np.sum(tr.out_end - tr.out_begin + 1))
+    row = {"config": "c4reuse", "n_traj": tr.n_traj, "n_steps": n_steps, "chi": chi,
+           "useful_traj_steps": useful, "unshared_traj_steps": int(tr.n_traj * (n_steps + 1))}
+    ref = None
+    for mode in ("0", "1"):
+        os.environ["PQD_BRANCH"] = mode
+        plan = engine.Plan(systems, grid, rho0, ops, tr, pt=pt)
+        os.environ.pop("PQD_BRANCH")
+        plan.execute()
+        plan.synchronize()
+        plan.timing(reset=True)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            plan.execute()
+        plan.synchronize()
+        el = (time.perf_counter() - t0) / steps
+        ms_free, ms_sweep, _ = plan.timing(reset=True)
+        out = np.concatenate([r.ravel() for r in plan.download()])
+        if ref is None:
+            ref = out
+        row["shared" if mode == "1" else "unshared"] = {
+            "executed_traj_steps": plan.traj_steps(), "wall_ms_per_launch": el * 1e3, "sweep_ms": ms_sweep,
+            "free_prop_ms": ms_free, "useful_traj_steps_per_s": useful / el,
+            "max_rel_diff_vs_unshared": float(np.max(np.abs(out - ref)) / np.max(np.abs(ref)))}
+    return row
+
+
 def run_c5dm(steps, n_e0=2, bxs=(0.0, 1.0, 2.0, 4.0), tend=400.0):
     import tempfile
     from pyaceqd_amd import opgrammar, pt as ptmod
@@ -178,7 +225,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     args = ap.parse_args()
     for name in args.configs.split(","):
-        print(json.dumps(run_c5dm(args.steps) if name == "c5dm" else run(name, args.steps)), flush=True)
+        special = {"c5dm": run_c5dm, "c4reuse": run_c4reuse}
+        print(json.dumps(special[name](args.steps) if name in special else run(name, args.steps)), flush=True)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,64 @@
+"""AddressSanitizer runs of native code (SURVEY.md §5 race/memory checks).
+
+CPU suite: the oracle's C sources built with -fsanitize=address (oracle/Makefile liboracle_asan.so) and loaded into a
+python with libasan preloaded; the oracle's golden and physics tests run on it in a subprocess and must finish with no
+ASan report. GPU: the host side of libpqd built with ASan on the host code only (hipcc -Xarch_host -fsanitize=address,
+pyaceqd_amd/csrc/Makefile `asan`; the device code is not instrumented) runs the C-ABI and a set of parity tests."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _libasan():
+    try:
+        p = subprocess.run(["gcc", "-print-file-name=libasan.so"], capture_output=True, text=True, timeout=30).stdout
+    except (OSError, subprocess.SubprocessError):
+        return None
+    p = p.strip()
+    return p if p and os.path.isabs(p) and os.path.exists(p) else None
+
+
+def _clang_asan_rt():
+    import glob
+    c = sorted(glob.glob("/opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so"))
+    return c[-1] if c else None
+
+
+def _run_under_asan(lib_env, tests, timeout, asan=None):
+    asan = asan or _libasan()
+    if asan is None:
+        pytest.skip("no libasan in this toolchain")
+    env = dict(os.environ, LD_PRELOAD=asan, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", **lib_env)
+    r = subprocess.run([sys.executable, "-m", "pytest", *tests, "-q", "-x", "-p", "no:cacheprovider"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=timeout)
+    out = r.stdout + r.stderr
+    msg = out if len(out) < 8000 else out[:5000] + "\n...\n" + out[-3000:]
+    assert "AddressSanitizer" not in out, msg
+    assert r.returncode == 0, msg
+    return out
+
+
+def test_oracle_under_asan():
+    lib = os.path.join(REPO, "oracle", "liboracle_asan.so")
+    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "oracle"), "liboracle_asan.so"])
+    env = dict(os.environ, LD_PRELOAD=_libasan() or "", ASAN_OPTIONS="detect_leaks=0", PQD_ORACLE_LIB=lib)
+    which = subprocess.run([sys.executable, "-c", "from oracle import oracle; oracle.lib(); print(oracle.LIB)"],
+                           cwd=REPO, env=env, capture_output=True, text=True, timeout=120)
+    assert which.stdout.strip().endswith("liboracle_asan.so"), which.stdout + which.stderr
+    out = _run_under_asan({"PQD_ORACLE_LIB": lib}, ["tests/test_oracle_golden.py", "tests/test_oracle_physics.py"], 600)
+    assert "passed" in out
+
+
+@pytest.mark.gpu
+def test_libpqd_host_code_under_asan():
+    lib = os.path.join(REPO, "pyaceqd_amd", "libpqd_asan.so")
+    if not os.path.exists(lib):
+        pytest.skip("libpqd_asan.so not built (make -C pyaceqd_amd/csrc asan)")
+    # hipcc's host compiler is clang: its ASan runtime, not gcc's libasan. torch is not imported in the subprocess
+    # (its HIP initialisation aborts under the preloaded runtime); these tests drive libpqd through ctypes only
+    _run_under_asan({"PQD_LIB": lib}, ["tests/test_gpu_quad.py", "tests/test_gpu_robustness.py",
+                                       "tests/test_gpu_branching.py"], 900, asan=_clang_asan_rt())
