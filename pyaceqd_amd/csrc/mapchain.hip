@@ -8,6 +8,7 @@
 // 64 / N2 trajectories, lane (traj, r) owns row r of that trajectory's Liouville vector.
 // One wave per workgroup, so every __syncthreads() is a single s_barrier.
 #include "pqd_common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -134,6 +135,93 @@ __global__ __launch_bounds__(64) void mc_tau_kernel(MapChainParams p) {
             if (jj + j_start == p.n_tb + 1) { j_start = 0; jj = 1; use_dm2 = 0; }
         }
     }
+}
+
+// tau sweeps, software-pipelined: the map rows of step k + PFD are loaded into registers while step k computes
+// (the sweep is a chain of dependent map-vector products whose maps are inputs, so their L2/HBM latency is hidden
+// behind PFD steps of arithmetic); the loop is unrolled by PFD so the register ring needs no moves, and every load is
+// unconditional (past the last step the lookahead state re-reads a valid map) so the compiler's wait counts stay
+// exact. x is double-buffered in LDS (one barrier per step); lane r keeps its own weighted term, lane 0 of each
+// trajectory sums them. Same map sequence and arithmetic as mc_tau_kernel (kept as PQD_MC_PIPE=0).
+template <int N2, int PFD>
+__global__ __launch_bounds__(64) void mc_tau_pipe_kernel(MapChainParams p) {
+    constexpr int TPW = 64 / N2;
+    __shared__ double2 xs[2][64], ts[64];
+    const int lane = threadIdx.x;
+    const int dim = p.dim;
+    const int tl = lane / N2, r = lane - (lane / N2) * N2;
+    const int i = blockIdx.x * TPW + tl;
+    const bool act = (tl < TPW) && (i < p.n_t);
+    const size_t m2 = (size_t)N2 * N2;
+    double2 w = c_zero();
+    if (act) {
+        const int a = r / dim, b = r % dim;
+        w = (p.mode == 2) ? p.opB[r] : p.opB[a + b * dim];
+        xs[0][lane] = p.rho_buf[(size_t)i * N2 + r];
+    }
+    // lookahead map state (the Fortran counters), advanced once per issued map
+    int jj = act ? p.j_arr[i] : 1;
+    int j_start = 0, use_dm2 = 1, kl = 2;
+    if (p.mode == 2) { j_start = jj; jj = 1; }
+    const int ncol = p.n_tau + 1;
+    auto map_now = [&]() -> const double2* {
+        if (!act || kl > ncol) return p.mode == 0 ? p.dmA : (p.mode == 1 ? p.dm_s : p.dm_s);
+        if (p.mode == 0) return p.dmA + (size_t)(jj - 2 + kl - 1) * m2;
+        if (p.mode == 1) return (jj <= p.n_map) ? p.dmA + (size_t)(jj - 1) * m2 : p.dm_s;
+        if (jj <= p.n_map) {
+            if (use_dm2)
+                return (i < p.n_tauc) ? p.dmT + m2 * ((size_t)i + (size_t)p.n_tauc * (jj - 1))
+                                      : p.dmB + (size_t)(jj - 1) * m2;
+            return p.dmA + (size_t)(jj - 1) * m2;
+        }
+        return p.dm_s;
+    };
+    auto advance = [&]() {
+        if (p.mode == 1) {
+            jj = jj + 1;
+            if (jj == p.n_tb + 1) jj = 1;
+        } else if (p.mode == 2) {
+            jj = jj + 1;
+            if (jj + j_start == p.n_tb + 1) { j_start = 0; jj = 1; use_dm2 = 0; }
+        }
+        ++kl;
+    };
+    double2 am[PFD][N2];
+    auto load_row = [&](int sl) {
+        const double2* A = map_now() + r;
+#pragma unroll
+        for (int c = 0; c < N2; ++c) am[sl][c] = A[c * N2];
+        advance();
+    };
+#pragma unroll
+    for (int sl = 0; sl < PFD; ++sl) load_row(sl);
+    __syncthreads();
+    int cur = 0;
+    auto step = [&](int sl, int k) {
+        const double2* x = xs[cur] + tl * N2;
+        double2 y = c_zero();
+#pragma unroll
+        for (int c = 0; c < N2; ++c) c_fma(y, am[sl][c], x[c]);
+        load_row(sl);  // the map of step k + PFD into the slot just used
+        xs[cur ^ 1][lane] = y;
+        ts[lane] = c_mul(w, y);
+        __syncthreads();
+        if (act && r == 0) {
+            double2 s = c_zero();
+#pragma unroll
+            for (int q = 0; q < N2; ++q) s = c_add(s, ts[tl * N2 + q]);
+            p.result[(size_t)i + (size_t)(k - 1) * p.n_t] = s;
+        }
+        cur ^= 1;
+    };
+    int k = 2;
+    for (; k + PFD - 1 <= ncol; k += PFD) {
+#pragma unroll
+        for (int sl = 0; sl < PFD; ++sl) step(sl, k + sl);
+    }
+#pragma unroll
+    for (int sl = 0; sl < PFD; ++sl)
+        if (k + sl <= ncol) step(sl, k + sl);
 }
 
 __global__ __launch_bounds__(64) void propagate_tau_kernel(const double2* dm, const double2* rho0, int N2,
@@ -319,7 +407,19 @@ hipError_t launch_mapchain(const MapChainParams& p, hipStream_t s) {
     if (e != hipSuccess) return e;
     const int TPW = 64 / p.N2;
     const int nblk = (p.n_t + TPW - 1) / TPW;
-    if (nblk > 0 && p.n_tau > 0) hipLaunchKernelGGL(mc_tau_kernel, dim3(nblk), dim3(64), 0, s, p);
+    if (nblk <= 0 || p.n_tau <= 0) return hipGetLastError();
+    const char* pe = getenv("PQD_MC_PIPE");
+    if (!(pe && atoi(pe) == 0)) {
+        switch (p.N2) {
+            case 4: hipLaunchKernelGGL((mc_tau_pipe_kernel<4, 4>), dim3(nblk), dim3(64), 0, s, p); return hipGetLastError();
+            case 9: hipLaunchKernelGGL((mc_tau_pipe_kernel<9, 2>), dim3(nblk), dim3(64), 0, s, p); return hipGetLastError();
+            case 16: hipLaunchKernelGGL((mc_tau_pipe_kernel<16, 2>), dim3(nblk), dim3(64), 0, s, p); return hipGetLastError();
+            case 25: hipLaunchKernelGGL((mc_tau_pipe_kernel<25, 1>), dim3(nblk), dim3(64), 0, s, p); return hipGetLastError();
+            case 36: hipLaunchKernelGGL((mc_tau_pipe_kernel<36, 1>), dim3(nblk), dim3(64), 0, s, p); return hipGetLastError();
+            default: break;
+        }
+    }
+    hipLaunchKernelGGL(mc_tau_kernel, dim3(nblk), dim3(64), 0, s, p);
     return hipGetLastError();
 }
 

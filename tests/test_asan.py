@@ -2,8 +2,11 @@
 
 CPU suite: the oracle's C sources built with -fsanitize=address (oracle/Makefile liboracle_asan.so) and loaded into a
 python with libasan preloaded; the oracle's golden and physics tests run on it in a subprocess and must finish with no
-ASan report. GPU: the host side of libpqd built with ASan on the host code only (hipcc -Xarch_host -fsanitize=address,
-pyaceqd_amd/csrc/Makefile `asan`; the device code is not instrumented) runs the C-ABI and a set of parity tests."""
+ASan report. libpqd's host code built with ASan on the host code only (hipcc -Xarch_host -fsanitize=address,
+pyaceqd_amd/csrc/Makefile `asan`; device code not instrumented) runs the C-ABI tests without a device (argument
+checks, error paths, symbol table). With a GPU visible the HIP runtime aborts at initialisation under a preloaded ASan
+runtime (measured on the MI355X box: `Fatal Python error: Aborted` in pqd_ctx_create, no ASan report; XNACK-on runs,
+which ROCm's ASan support needs, are not available there), so that run is CPU-only."""
 import os
 import subprocess
 import sys
@@ -53,12 +56,12 @@ def test_oracle_under_asan():
     assert "passed" in out
 
 
-@pytest.mark.gpu
 def test_libpqd_host_code_under_asan():
     lib = os.path.join(REPO, "pyaceqd_amd", "libpqd_asan.so")
     if not os.path.exists(lib):
         pytest.skip("libpqd_asan.so not built (make -C pyaceqd_amd/csrc asan)")
-    # hipcc's host compiler is clang: its ASan runtime, not gcc's libasan. torch is not imported in the subprocess
-    # (its HIP initialisation aborts under the preloaded runtime); these tests drive libpqd through ctypes only
-    _run_under_asan({"PQD_LIB": lib}, ["tests/test_gpu_quad.py", "tests/test_gpu_robustness.py",
-                                       "tests/test_gpu_branching.py"], 900, asan=_clang_asan_rt())
+    if os.path.exists("/dev/kfd"):
+        pytest.skip("a GPU is visible: the HIP runtime aborts under a preloaded ASan runtime (module docstring)")
+    # hipcc's host compiler is clang: its ASan runtime, not gcc's libasan
+    out = _run_under_asan({"PQD_LIB": lib}, ["tests/test_capi.py"], 600, asan=_clang_asan_rt())
+    assert "passed" in out
