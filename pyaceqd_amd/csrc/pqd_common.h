@@ -54,6 +54,7 @@ struct FreePropParams {
 struct SweepParams {
     const double2* M;        // 2*n_steps*N2*N2 free propagators
     const double2* Q;        // PT slices n_slices*D*CHI*CHI (chi padded to CHI)
+    const double* Qsum;      // Re + Im of Q (N2 = 4 PTs: the quad kernel's 3M operand), else NULL
     int D;
     const int* sched;        // n_steps
     const double2* closure;  // n_slices*CHI
@@ -178,4 +179,5 @@ hipError_t launch_split(int N2, int CHI, int n_traj, const SweepParams& p, doubl
 bool sweep_supported(int N2, int CHI);
 // the register-resident TLS sweep (pt_quad.hip): four trajectories per block, CHI/16 waves each
 bool quad_supported(int N2, int CHI);
-hipError_t launch_quad(int CHI, int n_quads, int qpw, const SweepParams& p, hipStream_t s);
+// ncg: 4-column groups per wave, 4 (strips of 16 columns, one wave per SIMD) or 2 (strips of 8, two waves per SIMD)
+hipError_t launch_quad(int CHI, int n_quads, int qpw, int ncg, const SweepParams& p, hipStream_t s);

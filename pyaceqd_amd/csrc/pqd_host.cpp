@@ -197,6 +197,7 @@ struct pqd_pt {
     pqd_ctx* ctx = nullptr;
     int dim = 0, chi = 0, CHI = 0, D = 0, n_slices = 0;
     DevBuf<double2> Q, closure, closure0, bond0;
+    DevBuf<double> Qsum;      // Re + Im of every slice element (the 3M operand of the TLS quad kernel; N2 = 4 only)
     DevBuf<int> gmap;
     std::vector<int> gmap_h;  // host copy: the plan derives its PT row units from it
 };
@@ -208,6 +209,7 @@ struct pqd_plan {
     bool split = false;  // small batch: one trajectory over N2 workgroups (pt_split.hip)
     bool quad = false;   // two-level system: register-resident quads (pt_quad.hip), blocks of BT = 4
     int qpw = 2;         // quads per workgroup (PQD_QPW)
+    int qcg = 4;         // 4-column groups per wave (PQD_QCG; auto: 2 when the quads do not fill the CUs)
     DevBuf<double2> Xs;
     DevBuf<unsigned> cnt, err;
     DevBuf<double2> L0, S, T, samples, M, Midle, F, W, rho0, ovec, sop, out;
@@ -355,6 +357,12 @@ int pqd_pt_create(pqd_ctx* ctx, int32_t dim, const pqd_pt_desc* d, pqd_pt** out)
     pt->ctx = ctx; pt->dim = dim; pt->chi = chi; pt->CHI = CHI; pt->D = d->D; pt->n_slices = d->n_slices;
     pt->gmap_h.assign(d->gmap, d->gmap + N2);
     hipError_t e = pt->Q.upload(Q.data(), qn, ctx->stream);
+    if (e == hipSuccess && N2 == 4) {
+        std::vector<double> qs(qn);
+        for (size_t k = 0; k < qn; ++k) qs[k] = Q[k].x + Q[k].y;
+        e = pt->Qsum.upload(qs.data(), qn, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);  // qs goes out of scope
+    }
     if (e == hipSuccess) e = pt->closure.upload(cl.data(), cl.size(), ctx->stream);
     if (e == hipSuccess) e = pt->closure0.upload(c0.data(), CHI, ctx->stream);
     if (e == hipSuccess) e = pt->bond0.upload(b0.data(), CHI, ctx->stream);
@@ -551,7 +559,7 @@ static void finalize_trunks(pqd_plan* P) {
 
 // the main batched sweep of a plan: quads (N2 = 4) or BT-trajectory workgroups
 static hipError_t launch_main(pqd_plan* P, hipStream_t s) {
-    if (P->quad) return launch_quad(P->CHI, P->n_blocks, P->qpw, P->sp, s);
+    if (P->quad) return launch_quad(P->CHI, P->n_blocks, P->qpw, P->qcg, P->sp, s);
     return launch_sweep(P->N2, P->CHI, P->BT, P->n_blocks, P->sp, s);
 }
 
@@ -851,7 +859,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     SweepParams& sp = P->sp;
     sp.M = P->M.p;
     if (pt) {
-        sp.Q = pt->Q.p; sp.D = pt->D; sp.closure = pt->closure.p; sp.closure0 = pt->closure0.p;
+        sp.Q = pt->Q.p; sp.Qsum = pt->Qsum.p; sp.D = pt->D; sp.closure = pt->closure.p; sp.closure0 = pt->closure0.p;
         sp.bond0 = pt->bond0.p; sp.gmap = pt->gmap.p;
     }
     sp.sched = P->sched.p; sp.rho0 = P->rho0.p; sp.n_out = n_out; sp.ovec = P->ovec.p;
@@ -892,6 +900,13 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     sp.woff = P->woff.p; sp.ev_start = P->ev_start.p; sp.ev = P->ev.p; sp.sop = P->sop.p; sp.out = P->out.p;
     sp.n_steps = ns;
     sp.n_blk = nb;
+    // quad kernel: with no more quads than CUs the step latency sets the time, and strips of 8 columns (twice the
+    // waves, two per SIMD) overlap one wave's round trips with the other's MFMAs (C2 single run 17.2 -> 13.1 ms);
+    // a full device runs the 16-column strips (measured equal on the 2,048-trajectory scan)
+    if (P->quad) {
+        P->qcg = nb <= n_cu ? 2 : 4;
+        if (const char* e = getenv("PQD_QCG")) P->qcg = atoi(e) == 2 ? 2 : 4;
+    }
     finalize_trunks(P);
     if (P->split) {
         HIPCHK(P->Xs.alloc((size_t)P->n_traj * 2 * N2 * P->CHI));

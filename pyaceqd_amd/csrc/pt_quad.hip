@@ -27,6 +27,7 @@
 // Semantics and shared-trunk activation (pqd_host.cpp branch_slots) are those of pt_sweep_kernel.
 #include "pqd_common.h"
 #include <climits>
+#include <cstdlib>
 #include <type_traits>
 
 namespace {
@@ -38,10 +39,11 @@ __device__ __forceinline__ double mfma4(double a, double b, double c) {
 // one column operator per trajectory (block t) applied to the C-layout state: R[cg] <- Op_t R[cg] where `mine`
 // (uniform per block t); `a` = this lane's operator element Op_t[alpha' = l & 3][alpha = l >> 4]. Every lane takes
 // part in the MFMAs (they read all 64 lanes); slots without an operator this round keep their values exactly.
-__device__ __forceinline__ void quad_col(double2 a, bool mine, double2 (&R)[4]) {
+template <int NCG>
+__device__ __forceinline__ void quad_col(double2 a, bool mine, double2 (&R)[NCG]) {
     const double as = a.x + a.y;
 #pragma unroll
-    for (int cg = 0; cg < 4; ++cg) {
+    for (int cg = 0; cg < NCG; ++cg) {
         const double bs = R[cg].x + R[cg].y;
         const double p1 = mfma4(a.x, R[cg].x, 0.0);
         const double p2 = mfma4(a.y, R[cg].y, 0.0);
@@ -69,9 +71,12 @@ __device__ __forceinline__ double2 quad_sum(double2 v) {  // sum over lanes l ^ 
     return v;
 }
 
-template <int CHI, int QPW, bool STAMP = false>
-__global__ __launch_bounds__(64 * QPW * (CHI / 16)) void pt_quad_kernel(SweepParams p) {
-    constexpr int NWG = CHI / 16;       // waves per quad (column strips of 16)
+// NCG = 4-column groups per wave: 4 (strips of 16 columns, one wave per SIMD) or 2 (strips of 8, twice the waves,
+// two per SIMD so one wave's LDS round trips and barrier hide behind the other's MFMAs)
+template <int CHI, int QPW, bool STAMP = false, int NCG = 4>
+__global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : 1) void pt_quad_kernel(SweepParams p) {
+    constexpr int CW = 4 * NCG;         // columns per wave
+    constexpr int NWG = CHI / CW;       // waves per quad (column strips of CW)
     constexpr int KS = CHI / 4;         // k-steps of the contraction
     constexpr int RS = CHI + 1;         // LDS row stride (double2)
     constexpr int QST = 16 * RS;        // one quad's rows (t, alpha)
@@ -125,17 +130,17 @@ __global__ __launch_bounds__(64 * QPW * (CHI / 16)) void pt_quad_kernel(SweepPar
     if (n_hi < 0 || n_lo == INT_MAX) return;  // whole workgroup empty
 
     double2* stq = smem + q * QST;        // + parity * QPW * QST
-    const int crow = (4 * lt + la) * RS + 16 * h + lc;                     // C-layout element (+ 4 cg)
+    const int crow = (4 * lt + la) * RS + CW * h + lc;                     // C-layout element (+ 4 cg)
     const int arow = (4 * (lane & 3) + ((lane >> 2) & 3)) * RS + (lane >> 4);  // A-layout element (+ 4 ks)
-    const int drow = (4 * (lane >> 4) + ((lane >> 2) & 3)) * RS + 16 * h + lc;  // D-layout element (+ 4 cg)
+    const int drow = (4 * (lane >> 4) + ((lane >> 2) & 3)) * RS + CW * h + lc;  // D-layout element (+ 4 cg)
 
     // ---- initial augmented states (slots active from step 0), before-MTOs at step 0
-    double2 R[4];
+    double2 R[NCG];
     {
         const double2 r0 = p.rho0[la];
 #pragma unroll
-        for (int cg = 0; cg < 4; ++cg)
-            R[cg] = (traj >= 0 && act == 0) ? c_mul(r0, p.bond0[16 * h + 4 * cg + lc]) : c_zero();
+        for (int cg = 0; cg < NCG; ++cg)
+            R[cg] = (traj >= 0 && act == 0) ? c_mul(r0, p.bond0[CW * h + 4 * cg + lc]) : c_zero();
     }
     int4 evn = ev_cur < ev_lim ? p.ev[ev_cur] : make_int4(INT_MAX, 0, 0, 0);
     {
@@ -161,21 +166,28 @@ __global__ __launch_bounds__(64 * QPW * (CHI / 16)) void pt_quad_kernel(SweepPar
     // it), and the common path (fused steps, no MTO, no activation) is straight-line, so the compiler's wait counts
     // stay exact and never drain the prefetched loads early.
     const int bl_a = (lane >> 2) & 3, bl_k = lane >> 4;   // B-layout alpha, k'
-    const size_t qoff = (size_t)p.gmap[bl_a] * CHI * CHI + (size_t)bl_k * CHI + 16 * h + lc;
+    const size_t qoff = (size_t)p.gmap[bl_a] * CHI * CHI + (size_t)bl_k * CHI + CW * h + lc;
     const size_t sstride = (size_t)p.D * CHI * CHI;
-    double2 B[KS][4];
+    double2 B[KS][NCG];
+    // Re + Im of B (precomputed per PT: the 3M operand without VALU adds per step) where the registers allow it
+    constexpr bool PRESUM = CHI == 16;
+    double Bs[PRESUM ? KS : 1][PRESUM ? NCG : 1];
     auto load_slices = [&](int s) {
         const double2* Qs = p.Q + (size_t)s * sstride + qoff;
+        const double* Qm = p.Qsum + (size_t)s * sstride + qoff;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-            for (int cg = 0; cg < 4; ++cg) B[ks][cg] = Qs[(size_t)4 * ks * CHI + 4 * cg];
+            for (int cg = 0; cg < NCG; ++cg) {
+                B[ks][cg] = Qs[(size_t)4 * ks * CHI + 4 * cg];
+                if constexpr (PRESUM) Bs[ks][cg] = Qm[(size_t)4 * ks * CHI + 4 * cg];
+            }
     };
-    double2 cl[4];
+    double2 cl[NCG];
     auto load_closure = [&](int s) {  // s < 0: closure0
         const double2* cv = s < 0 ? p.closure0 : p.closure + (size_t)s * CHI;
 #pragma unroll
-        for (int cg = 0; cg < 4; ++cg) cl[cg] = cv[16 * h + 4 * cg + lc];
+        for (int cg = 0; cg < NCG; ++cg) cl[cg] = cv[CW * h + 4 * cg + lc];
     };
     const double2* Fp = fuse ? p.F + (size_t)sys * p.f_stride : p.M;  // unfused plans: the ring reads p.M[0]
     const double2* Wp = fuse ? p.W + (size_t)sys2 * p.w_stride : p.M;
@@ -194,9 +206,18 @@ __global__ __launch_bounds__(64 * QPW * (CHI / 16)) void pt_quad_kernel(SweepPar
     fpre[0] = ldF(n0); ldW(0, n0); sr[0] = ldS(n0 + 1);
     fpre[1] = ldF(n0 + 1); ldW(1, n0 + 1); sr[1] = ldS(n0 + 2);
 
-    // one step; S = ring slot of step n. Returns true when the workgroup is done.
-    auto step = [&](auto S_, const int n) -> bool {
-        constexpr int S = decltype(S_)::value;
+    // end of step n: the ring moves one step (slot 0 = step n + 1, loaded a step ago) and slot 1 fetches step n + 2
+    auto shift_ring = [&](int n) {
+        fpre[0] = fpre[1];
+        wv[0] = wv[1];
+        sr[0] = sr[1];
+        fpre[1] = ldF(n + 2);
+        ldW(1, n + 2);
+        sr[1] = ldS(n + 3);
+    };
+    // one step (ring slot 0 = step n). Returns true when the workgroup is done.
+    auto step = [&](const int n) -> bool {
+        constexpr int S = 0;
         auto stamp = [&](int k) {
             if constexpr (STAMP) {
                 if (blockIdx.x == 0 && threadIdx.x == 0 && n >= 1000 && n < 1016)
@@ -211,19 +232,19 @@ __global__ __launch_bounds__(64 * QPW * (CHI / 16)) void pt_quad_kernel(SweepPar
         // ------------------------------------------------ shared-trunk activations at the top of step n
         if (n == next_act) {
             const int sl = 16 * la + 4 * (src >= 0 ? src : 0) + lc;
-            double2 Rs[4];
+            double2 Rs[NCG];
 #pragma unroll
-            for (int cg = 0; cg < 4; ++cg) Rs[cg] = make_double2(__shfl(R[cg].x, sl), __shfl(R[cg].y, sl));
+            for (int cg = 0; cg < NCG; ++cg) Rs[cg] = make_double2(__shfl(R[cg].x, sl), __shfl(R[cg].y, sl));
             const bool fzs = __shfl((int)fz, sl) != 0;
             if (act == n) {
                 if (src >= 0) {
 #pragma unroll
-                    for (int cg = 0; cg < 4; ++cg) R[cg] = Rs[cg];
+                    for (int cg = 0; cg < NCG; ++cg) R[cg] = Rs[cg];
                     fz = fzs;
                 } else if (src <= -2) {
-                    const double2* ck = p.ck + (size_t)(-2 - src) * 4 * CHI + (size_t)la * CHI + 16 * h + lc;
+                    const double2* ck = p.ck + (size_t)(-2 - src) * 4 * CHI + (size_t)la * CHI + CW * h + lc;
 #pragma unroll
-                    for (int cg = 0; cg < 4; ++cg) R[cg] = ck[4 * cg];
+                    for (int cg = 0; cg < NCG; ++cg) R[cg] = ck[4 * cg];
                     fz = true;
                 }
             }
@@ -242,7 +263,7 @@ __global__ __launch_bounds__(64 * QPW * (CHI / 16)) void pt_quad_kernel(SweepPar
         if (need) {
             double2 part = c_zero();
 #pragma unroll
-            for (int cg = 0; cg < 4; ++cg) c_fma(part, R[cg], cl[cg]);
+            for (int cg = 0; cg < NCG; ++cg) c_fma(part, R[cg], cl[cg]);
             part = quad_sum(part);
             if (lc == 0) rpp[h * 16 + 4 * lt + la] = part;
         }
@@ -282,7 +303,7 @@ __global__ __launch_bounds__(64 * QPW * (CHI / 16)) void pt_quad_kernel(SweepPar
         stamp(2);
         // ------------------------------------------------ exchange: this strip's columns -> rows of every wave
 #pragma unroll
-        for (int cg = 0; cg < 4; ++cg) st[crow + 4 * cg] = R[cg];
+        for (int cg = 0; cg < NCG; ++cg) st[crow + 4 * cg] = R[cg];
         if constexpr (NWG > 1 || QPW > 1) __syncthreads();
         else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         stamp(3);
@@ -306,28 +327,28 @@ __global__ __launch_bounds__(64 * QPW * (CHI / 16)) void pt_quad_kernel(SweepPar
         if (n >= n_hi) return true;
         if (n >= q_hi) return false;  // this quad is done; the others still step (next: the !qlive branch)
         // ------------------------------------------------ PT contraction of step n (3M, all rows in one stream)
-        double2 D[4];
+        double2 D[NCG];
         if (!(p.ablate & 1)) {
             double2 A[KS];
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) A[ks] = st[arow + 4 * ks];
-            double p1[4] = {0, 0, 0, 0}, p2[4] = {0, 0, 0, 0}, p3[4] = {0, 0, 0, 0};
+            double p1[NCG] = {}, p2[NCG] = {}, p3[NCG] = {};
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
                 const double as = A[ks].x + A[ks].y;
 #pragma unroll
-                for (int cg = 0; cg < 4; ++cg) {
+                for (int cg = 0; cg < NCG; ++cg) {
                     p1[cg] = mfma4(A[ks].x, B[ks][cg].x, p1[cg]);
                     p2[cg] = mfma4(A[ks].y, B[ks][cg].y, p2[cg]);
-                    p3[cg] = mfma4(as, B[ks][cg].x + B[ks][cg].y, p3[cg]);
+                    p3[cg] = mfma4(as, PRESUM ? Bs[PRESUM ? ks : 0][PRESUM ? cg : 0] : B[ks][cg].x + B[ks][cg].y, p3[cg]);
                 }
             }
 #pragma unroll
-            for (int cg = 0; cg < 4; ++cg) D[cg] = make_double2(p1[cg] - p2[cg], p3[cg] - p1[cg] - p2[cg]);
+            for (int cg = 0; cg < NCG; ++cg) D[cg] = make_double2(p1[cg] - p2[cg], p3[cg] - p1[cg] - p2[cg]);
         } else {
             // diagnostics: the rows unchanged (read back in D-layout)
 #pragma unroll
-            for (int cg = 0; cg < 4; ++cg) D[cg] = st[drow + 4 * cg];
+            for (int cg = 0; cg < NCG; ++cg) D[cg] = st[drow + 4 * cg];
         }
         if constexpr (STAMP) {  // wait for the contraction's results before the stamp
             if (blockIdx.x == 0 && threadIdx.x == 0 && n >= 1000 && n < 1016 && D[0].x == 12345.678) g_quad_stamps[255] = 1;
@@ -336,10 +357,8 @@ __global__ __launch_bounds__(64 * QPW * (CHI / 16)) void pt_quad_kernel(SweepPar
         // operands ahead, in the order they are needed (loads complete in order): F/W and the schedule of step n + 2
         // into the slot this step used, then (if the slice changes) the closure and the slices of step n + 1
         {
-            const int s1 = __builtin_amdgcn_readfirstlane(sr[S]);  // sched[n + 1]
-            fpre[S] = ldF(n + 2);
-            ldW(S, n + 2);
-            sr[S] = ldS(n + 3);
+            const int s1 = __builtin_amdgcn_readfirstlane(sr[0]);  // sched[n + 1]
+            shift_ring(n);
             if (q_cur != c_cur) { load_closure(q_cur); c_cur = q_cur; }  // closure of step n + 1: sched[n]
             if (s1 != q_cur) { load_slices(s1); q_cur = s1; }
         }
@@ -348,10 +367,10 @@ __global__ __launch_bounds__(64 * QPW * (CHI / 16)) void pt_quad_kernel(SweepPar
         {
             double2* sn = stq + (par ^ 1) * QPW * QST;
 #pragma unroll
-            for (int cg = 0; cg < 4; ++cg) sn[drow + 4 * cg] = D[cg];
+            for (int cg = 0; cg < NCG; ++cg) sn[drow + 4 * cg] = D[cg];
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-            for (int cg = 0; cg < 4; ++cg) R[cg] = sn[crow + 4 * cg];
+            for (int cg = 0; cg < NCG; ++cg) R[cg] = sn[crow + 4 * cg];
         }
         stamp(7);
         // ------------------------------------------------ column phase B: M_b(n) and before-MTOs at n+1 unless fused
@@ -387,10 +406,10 @@ __global__ __launch_bounds__(64 * QPW * (CHI / 16)) void pt_quad_kernel(SweepPar
     // matrix cores, exchange + barrier, A-operand reads, the contraction.
     auto fast_ok = [&](int n) -> bool {
         return n != next_act && n < q_hi && n < n_hi && fuse && NO <= 4 && !(p.ablate & 31) &&
-               !__ballot(traj >= 0 && n >= act && (!fz || evn.x == n || evn.x == n + 1));
+               !__ballot(traj >= 0 && (n < act || !fz || evn.x == n || evn.x == n + 1));
     };
-    auto fast = [&](auto S_, const int n) {
-        constexpr int S = decltype(S_)::value;
+    auto fast = [&](const int n) {
+        constexpr int S = 0;
         auto stamp = [&](int k) {
             if constexpr (STAMP) {
                 if (blockIdx.x == 0 && threadIdx.x == 0 && n >= 1000 && n < 1016)
@@ -401,19 +420,18 @@ __global__ __launch_bounds__(64 * QPW * (CHI / 16)) void pt_quad_kernel(SweepPar
         const int par = n & 1;
         double2* st = stq + par * QPW * QST;
         double2* rpp = rp + (par * QPW + q) * NWG * 16;
-        const bool on = traj >= 0 && n >= act;
         // closure partial of this strip (outputs at step n) beside the column operator F(n)
         {
             double2 part = c_zero();
 #pragma unroll
-            for (int cg = 0; cg < 4; ++cg) c_fma(part, R[cg], cl[cg]);
+            for (int cg = 0; cg < NCG; ++cg) c_fma(part, R[cg], cl[cg]);
             part = quad_sum(part);
             if (lc == 0) rpp[h * 16 + 4 * lt + la] = part;
         }
-        quad_col(fpre[S], on, R);
+        quad_col(fpre[S], true, R);  // every valid slot is active (empty slots hold zeros)
         stamp(1);
 #pragma unroll
-        for (int cg = 0; cg < 4; ++cg) st[crow + 4 * cg] = R[cg];
+        for (int cg = 0; cg < NCG; ++cg) st[crow + 4 * cg] = R[cg];
         if constexpr (NWG > 1 || QPW > 1) __syncthreads();
         else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         stamp(2);
@@ -421,15 +439,15 @@ __global__ __launch_bounds__(64 * QPW * (CHI / 16)) void pt_quad_kernel(SweepPar
         double2 A[KS];
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) A[ks] = st[arow + 4 * ks];
-        double p1[4] = {0, 0, 0, 0}, p2[4] = {0, 0, 0, 0}, p3[4] = {0, 0, 0, 0};
+        double p1[NCG] = {}, p2[NCG] = {}, p3[NCG] = {};
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             const double as = A[ks].x + A[ks].y;
 #pragma unroll
-            for (int cg = 0; cg < 4; ++cg) {
+            for (int cg = 0; cg < NCG; ++cg) {
                 p1[cg] = mfma4(A[ks].x, B[ks][cg].x, p1[cg]);
                 p2[cg] = mfma4(A[ks].y, B[ks][cg].y, p2[cg]);
-                p3[cg] = mfma4(as, B[ks][cg].x + B[ks][cg].y, p3[cg]);
+                p3[cg] = mfma4(as, PRESUM ? Bs[PRESUM ? ks : 0][PRESUM ? cg : 0] : B[ks][cg].x + B[ks][cg].y, p3[cg]);
             }
         }
         // traces of step n (strip 0; every slot is fused: W(n) rows), stored inside each trajectory's window
@@ -442,14 +460,12 @@ __global__ __launch_bounds__(64 * QPW * (CHI / 16)) void pt_quad_kernel(SweepPar
                 p.out[wo2 + (long long)(n - wb2) * NO + k2] = x;
         }
         // ring loads of step n + 2 into the slot this step used
-        const int s1 = __builtin_amdgcn_readfirstlane(sr[S]);  // sched[n + 1]
-        fpre[S] = ldF(n + 2);
-        ldW(S, n + 2);
-        sr[S] = ldS(n + 3);
+        const int s1 = __builtin_amdgcn_readfirstlane(sr[0]);  // sched[n + 1]
+        shift_ring(n);
         stamp(3);
-        double2 D[4];
+        double2 D[NCG];
 #pragma unroll
-        for (int cg = 0; cg < 4; ++cg) D[cg] = make_double2(p1[cg] - p2[cg], p3[cg] - p1[cg] - p2[cg]);
+        for (int cg = 0; cg < NCG; ++cg) D[cg] = make_double2(p1[cg] - p2[cg], p3[cg] - p1[cg] - p2[cg]);
         if constexpr (STAMP) {  // wait for the contraction's results before the stamp
             if (blockIdx.x == 0 && threadIdx.x == 0 && n >= 1000 && n < 1016 && D[0].x == 12345.678) g_quad_stamps[255] = 1;
         }
@@ -458,10 +474,10 @@ __global__ __launch_bounds__(64 * QPW * (CHI / 16)) void pt_quad_kernel(SweepPar
         {
             double2* sn = stq + (par ^ 1) * QPW * QST;
 #pragma unroll
-            for (int cg = 0; cg < 4; ++cg) sn[drow + 4 * cg] = D[cg];
+            for (int cg = 0; cg < NCG; ++cg) sn[drow + 4 * cg] = D[cg];
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-            for (int cg = 0; cg < 4; ++cg) R[cg] = sn[crow + 4 * cg];
+            for (int cg = 0; cg < NCG; ++cg) R[cg] = sn[crow + 4 * cg];
         }
         stamp(5);
         // a new slice (or closure) for step n + 1 only when the schedule changes
@@ -469,31 +485,25 @@ __global__ __launch_bounds__(64 * QPW * (CHI / 16)) void pt_quad_kernel(SweepPar
         if (s1 != q_cur) { load_slices(s1); q_cur = s1; }
         stamp(6);
     };
-    using S0 = std::integral_constant<int, 0>;
-    using S1 = std::integral_constant<int, 1>;
-    for (int n = n0;; n += 2) {
-        // runs of fast step pairs in a loop of their own (one loop body: the compiler's wait counts stay exact)
-        while (fast_ok(n) && fast_ok(n + 1)) {
-            fast(S0{}, n);
-            fast(S1{}, n + 1);
-            n += 2;
+    for (int n = n0;; ++n) {
+        // runs of fast steps in a loop of their own (one loop body: the compiler's wait counts stay exact)
+        while (fast_ok(n)) {
+            fast(n);
+            ++n;
         }
-        if (fast_ok(n)) fast(S0{}, n);
-        else if (step(S0{}, n)) break;
-        if (fast_ok(n + 1)) fast(S1{}, n + 1);
-        else if (step(S1{}, n + 1)) break;
+        if (step(n)) break;
     }
 }
 
-template <int CHI, int QPW>
+template <int CHI, int QPW, int NCG>
 hipError_t launch_q(int n_quads, const SweepParams& p, hipStream_t s) {
-    constexpr int NWG = CHI / 16;
+    constexpr int NWG = CHI / (4 * NCG);
     const size_t lds = (size_t)(2 * QPW * 16 * (CHI + 1) + 2 * QPW * NWG * 16) * sizeof(double2);
     const int grid = (n_quads + QPW - 1) / QPW;
     if (p.ablate & 32)
-        hipLaunchKernelGGL((pt_quad_kernel<CHI, QPW, true>), dim3(grid), dim3(64 * QPW * NWG), lds, s, p);
+        hipLaunchKernelGGL((pt_quad_kernel<CHI, QPW, true, NCG>), dim3(grid), dim3(64 * QPW * NWG), lds, s, p);
     else
-        hipLaunchKernelGGL((pt_quad_kernel<CHI, QPW>), dim3(grid), dim3(64 * QPW * NWG), lds, s, p);
+        hipLaunchKernelGGL((pt_quad_kernel<CHI, QPW, false, NCG>), dim3(grid), dim3(64 * QPW * NWG), lds, s, p);
     return hipGetLastError();
 }
 
@@ -506,11 +516,15 @@ extern "C" int pqd_debug_quad_stamps(unsigned long long* out) {
 
 bool quad_supported(int N2, int CHI) { return N2 == 4 && (CHI == 16 || CHI == 32); }
 
-hipError_t launch_quad(int CHI, int n_quads, int qpw, const SweepParams& p, hipStream_t s) {
+hipError_t launch_quad(int CHI, int n_quads, int qpw, int ncg, const SweepParams& p, hipStream_t s) {
     if (n_quads <= 0) return hipSuccess;
     switch (CHI) {
-        case 16: return qpw >= 2 ? launch_q<16, 4>(n_quads, p, s) : launch_q<16, 1>(n_quads, p, s);
-        case 32: return qpw >= 2 ? launch_q<32, 2>(n_quads, p, s) : launch_q<32, 1>(n_quads, p, s);
+        case 16:
+            if (ncg == 2) return qpw >= 2 ? launch_q<16, 2, 2>(n_quads, p, s) : launch_q<16, 1, 2>(n_quads, p, s);
+            return qpw >= 2 ? launch_q<16, 4, 4>(n_quads, p, s) : launch_q<16, 1, 4>(n_quads, p, s);
+        case 32:
+            if (ncg == 2) return qpw >= 2 ? launch_q<32, 2, 2>(n_quads, p, s) : launch_q<32, 1, 2>(n_quads, p, s);
+            return qpw >= 2 ? launch_q<32, 2, 4>(n_quads, p, s) : launch_q<32, 1, 4>(n_quads, p, s);
         default: return hipErrorInvalidValue;
     }
 }

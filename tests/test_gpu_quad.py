@@ -27,9 +27,11 @@ def _run(systems, grid, rho0, ops, tr, pt):
 @pytest.mark.parametrize("chi", [8, 16, 32])
 @pytest.mark.parametrize("fuse", ["0", "1"])
 @pytest.mark.parametrize("qpw", ["1", "2"])
-def test_quad_vs_oracle(monkeypatch, chi, fuse, qpw):
+@pytest.mark.parametrize("qcg", ["2", "4"])
+def test_quad_vs_oracle(monkeypatch, chi, fuse, qpw, qcg):
     monkeypatch.setenv("PQD_FUSE", fuse)
     monkeypatch.setenv("PQD_QPW", qpw)
+    monkeypatch.setenv("PQD_QCG", qcg)
     monkeypatch.setenv("PQD_SPLIT", "0")
     N = 2
     systems = [H.random_system(N, n_steps=40, seed=60 + k)[0] for k in range(3)]
@@ -75,7 +77,9 @@ def _g2_sweep(n_t1, n_tau, seed):
 
 
 @pytest.mark.parametrize("mode", ["branch", "trunk", "none"])
-def test_quad_shared_trunks(monkeypatch, mode):
+@pytest.mark.parametrize("qcg", ["2", "4"])
+def test_quad_shared_trunks(monkeypatch, mode, qcg):
+    monkeypatch.setenv("PQD_QCG", qcg)
     monkeypatch.setenv("PQD_SPLIT", "0")
     monkeypatch.setenv("PQD_BRANCH", "0" if mode == "none" else "1")
     monkeypatch.setenv("PQD_TRUNK", "1" if mode == "trunk" else "0")
