@@ -108,6 +108,10 @@ __global__ __launch_bounds__(256) void free_prop_kernel(FreePropParams p) {
     const int nsub = p.n_sub > 0 ? p.n_sub : 1;
     const double w = 0.5 * p.dt / nsub;
     double2* out = p.idle_pass ? p.Midle + (size_t)si * N2 * N2 : p.M + ((size_t)si * 2 * p.n_steps + m) * N2 * N2;
+    if (!p.idle_pass && p.win) {  // outside the pulse window: not stored (readers take Midle)
+        const int2 wn = p.win[si];
+        if (m < wn.x || m > wn.y) continue;
+    }
     if (!p.idle_pass && p.Midle && idle_half_step(sy, p.ta + n * p.dt + h * 0.5 * p.dt, w, nsub)) {
         const double2* src = p.Midle + (size_t)si * N2 * N2;
         for (int e = tid; e < N2 * N2; e += 256) out[e] = src[e];
@@ -220,17 +224,11 @@ __device__ __forceinline__ double2 grp_matmul4(double2 a, double2 b, int gb, int
     return acc;
 }
 
-__global__ __launch_bounds__(256) void free_prop4_kernel(FreePropParams p) {
-    const int tid = threadIdx.x;
-    const long long n_mat = p.idle_pass ? (long long)p.n_sys : (long long)p.n_sys * 2 * p.n_steps;
-    for (long long base = (long long)blockIdx.x * 16; base < n_mat; base += (long long)gridDim.x * 16) {
-    const long long mat = base + (tid >> 4);
-    const bool live = mat < n_mat;
-    const long long mc = live ? mat : n_mat - 1;  // dead lanes shadow the last matrix (no store)
-    const int si = p.idle_pass ? (int)mc : (int)(mc / (2 * p.n_steps));
-    const int m = p.idle_pass ? 0 : (int)(mc - (long long)si * 2 * p.n_steps);
+// one 4 x 4 propagator per 16-lane group: matrix (si, m) (m = half step; the idle pass: Midle of si). Dead groups
+// (live = false) shadow a live matrix of the same workgroup and store nothing
+__device__ __forceinline__ void fp4_matrix(const FreePropParams& p, int si, int m, bool live, int lane) {
     const int n = m >> 1, h = m & 1;
-    const int lane = tid & 63, gb = lane & ~15, e = lane & 15, i = e >> 2, j = e & 3;
+    const int gb = lane & ~15, e = lane & 15, i = e >> 2, j = e & 3;
     const FreePropSys sy = p.systems[si];
     const int nsub = p.n_sub > 0 ? p.n_sub : 1;
     const double w = 0.5 * p.dt / nsub;
@@ -239,7 +237,7 @@ __global__ __launch_bounds__(256) void free_prop4_kernel(FreePropParams p) {
     // shuffles below never mix copied and computed matrices of different groups
     if (!p.idle_pass && p.Midle && idle_half_step(sy, p.ta + n * p.dt + h * 0.5 * p.dt, w, nsub)) {
         if (live) out[e] = p.Midle[(size_t)si * 16 + e];
-        continue;
+        return;
     }
     double2 acc = c_zero();
     for (int js = 0; js < nsub; ++js) {
@@ -277,6 +275,90 @@ __global__ __launch_bounds__(256) void free_prop4_kernel(FreePropParams p) {
         acc = (js == 0) ? pm : grp_matmul4(pm, acc, gb, i, j);
     }
     if (live) out[e] = acc;
+}
+
+// main pass: one workgroup per p.chunk consecutive half steps of one system (16..128: 8 groups of 16 when the launch
+// has thousands of workgroups to spare, 1 for a single system), clipped to the system's pulse window once (one window
+// load per workgroup: a load per 16-matrix group made the out-of-window groups latency-bound, 1.5 ms of the TLS area
+// scan's 4 ms)
+static int fp4_chunk(const FreePropParams& p) {
+    const long long groups = (long long)p.n_sys * ((2LL * p.n_steps + 15) / 16);
+    long long g = groups / 8192;
+    if (const char* e = getenv("PQD_FP4_CHUNK")) return atoi(e);  // A/B (a multiple of 16)
+    return 16 * (int)(g < 1 ? 1 : (g > 8 ? 8 : g));
+}
+
+__global__ __launch_bounds__(256) void free_prop4_kernel(FreePropParams p) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    if (p.idle_pass) {
+        for (long long base = (long long)blockIdx.x * 16; base < p.n_sys; base += (long long)gridDim.x * 16) {
+            const long long mat = base + (tid >> 4);
+            const bool live = mat < p.n_sys;
+            fp4_matrix(p, (int)(live ? mat : p.n_sys - 1), 0, live, lane);
+        }
+        return;
+    }
+    const int nh = 2 * p.n_steps, CH = p.chunk, cps = (nh + CH - 1) / CH;
+    const long long nblk = (long long)p.n_sys * cps;
+    for (long long b = blockIdx.x; b < nblk; b += gridDim.x) {
+        // chunks rotate with the system: workgroups go to the 8 XCDs round-robin, so with cps a multiple of 8 the
+        // chunk at one time position (pulse centre: larger norms, more squarings) would land on one XCD for every
+        // system (C1 free propagators 3.8 -> 5.7 ms at 64/128-step chunks without the rotation)
+        const int si = (int)(b / cps), r = (int)(b - (long long)si * cps), ch = (r + si) % cps;
+        int lo = ch * CH, hi = (lo + CH < nh ? lo + CH : nh) - 1;
+        if (p.win) {  // outside the pulse window: not stored (readers take Midle)
+            const int2 wn = p.win[si];
+            lo = lo > wn.x ? lo : wn.x;
+            hi = hi < wn.y ? hi : wn.y;
+        }
+        for (int base = lo; base <= hi; base += 16) {
+            const int m = base + (tid >> 4);
+            const bool live = m <= hi;
+            fp4_matrix(p, si, live ? m : hi, live, lane);
+        }
+    }
+}
+
+// Pulse windows: win[s] = (first, last) half step of system s that is not idle (INT_MAX, -1 when all are). The idle
+// test is the builders' own, so a half step outside the window is exactly one the builders would have copied Midle
+// into. One workgroup per 256 consecutive half steps of one system: a block reduction, then one atomic min / max.
+__global__ __launch_bounds__(256) void free_win_init_kernel(int2* win, int n_sys) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n_sys) win[i] = make_int2(INT_MAX, -1);
+}
+
+__global__ __launch_bounds__(256) void free_win_kernel(FreePropParams p) {
+    __shared__ int s_lo[4], s_hi[4];
+    const int nh = 2 * p.n_steps, chunks = (nh + 255) / 256;
+    const long long nblk = (long long)p.n_sys * chunks;
+    const int nsub = p.n_sub > 0 ? p.n_sub : 1;
+    const double w = 0.5 * p.dt / nsub;
+    for (long long blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        const int si = (int)(blk / chunks);
+        const int m = (int)(blk - (long long)si * chunks) * 256 + (int)threadIdx.x;
+        int lo = INT_MAX, hi = -1;
+        if (m < nh) {
+            const FreePropSys sy = p.systems[si];
+            const int n = m >> 1, h = m & 1;
+            if (!idle_half_step(sy, p.ta + n * p.dt + h * 0.5 * p.dt, w, nsub)) lo = hi = m;
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const int a = __shfl_xor(lo, o), b = __shfl_xor(hi, o);
+            lo = a < lo ? a : lo;
+            hi = b > hi ? b : hi;
+        }
+        const int wv = threadIdx.x >> 6;
+        if ((threadIdx.x & 63) == 0) { s_lo[wv] = lo; s_hi[wv] = hi; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int k = 1; k < 4; ++k) { lo = s_lo[k] < lo ? s_lo[k] : lo; hi = s_hi[k] > hi ? s_hi[k] : hi; }
+            if (hi >= 0) {
+                atomicMin(&p.win[si].x, lo);
+                atomicMax(&p.win[si].y, hi);
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -309,9 +391,16 @@ __global__ __launch_bounds__(256) void fuse_steps_kernel(FuseParams p) {
     for (long long blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
     const int si = (int)(blk / p.n_steps), m = (int)(blk - (long long)si * p.n_steps) + 1;  // m = 1..n_steps
     const int tid = threadIdx.x;
-    const double2* Mb = p.M + ((size_t)si * 2 * p.n_steps + 2 * (m - 1) + 1) * N2 * N2;
+    int2 wn = make_int2(INT_MIN, INT_MAX);
+    if (p.win) wn = p.win[si];
+    const bool out_b = 2 * m - 1 < wn.x || 2 * m - 1 > wn.y, out_a = 2 * m < wn.x || 2 * m > wn.y;
+    if (out_b && out_a) continue;  // F(m) and W(m) are the idle ones (block-uniform)
+    // a half step outside the window is not stored: its propagator is Midle
+    const double2* Mb = out_b ? p.Midle + (size_t)si * N2 * N2
+                              : p.M + ((size_t)si * 2 * p.n_steps + 2 * (m - 1) + 1) * N2 * N2;
     if (m < p.n_steps) {
-        const double2* Ma = p.M + ((size_t)si * 2 * p.n_steps + 2 * m) * N2 * N2;
+        const double2* Ma = out_a ? p.Midle + (size_t)si * N2 * N2
+                                  : p.M + ((size_t)si * 2 * p.n_steps + 2 * m) * N2 * N2;
         double2* F = p.F + ((size_t)si * p.n_steps + m) * N2 * N2;
         for (int e = tid; e < N2 * N2; e += 256) {
             const int r = e / N2, c = e - (e / N2) * N2;
@@ -322,6 +411,7 @@ __global__ __launch_bounds__(256) void fuse_steps_kernel(FuseParams p) {
         }
     }
     double2* W = p.W + ((size_t)si * (p.n_steps + 1) + m) * p.n_out * N2;
+    if (!out_b)
     for (int e = tid; e < p.n_out * N2; e += 256) {
         const int k = e / N2, a = e - (e / N2) * N2;
         double2 acc = c_zero();
@@ -332,30 +422,76 @@ __global__ __launch_bounds__(256) void fuse_steps_kernel(FuseParams p) {
     }
 }
 
-// small N2: one thread per output element of every (system, step) — F(m) entries, then W(m) entries — instead of a
-// 256-thread workgroup per step with N2^2 + n_out N2 of its threads busy (N2 = 4: 24 of 256)
+// small N2: one thread per output element — F(m) entries, then W(m) entries — instead of a 256-thread workgroup per
+// step with N2^2 + n_out N2 of its threads busy (N2 = 4: 24 of 256). A workgroup takes FS_CHUNK steps of one system,
+// clipped to the steps whose F or W is stored (the pulse window) with one window load
+constexpr int FS_CHUNK = 64;
+
 template <int N2>
 __global__ __launch_bounds__(256) void fuse_steps_flat_kernel(FuseParams p) {
     const int E = N2 * N2 + p.n_out * N2;
-    const long long total = (long long)p.n_sys * p.n_steps * E;
+    const int cps = (p.n_steps + FS_CHUNK - 1) / FS_CHUNK;
+    const long long nblk = (long long)p.n_sys * cps;
+    for (long long bk = blockIdx.x; bk < nblk; bk += gridDim.x) {
+        const int si = (int)(bk / cps), ch = (int)(bk - (long long)si * cps);
+        int m_lo = 1 + ch * FS_CHUNK, m_hi = m_lo + FS_CHUNK - 1 < p.n_steps ? m_lo + FS_CHUNK - 1 : p.n_steps;
+        int2 wn = make_int2(INT_MIN, INT_MAX);
+        if (p.win) {
+            wn = p.win[si];
+            if (wn.y < 0) continue;  // no pulse at all: every F and W is the idle one
+            // F(m) is stored when 2m - 1 or 2m lies in [lo, hi], W(m) when 2m - 1 does: m in [ceil(lo/2), (hi+1)/2]
+            const int a = (wn.x + 1) >> 1, b = (wn.y + 1) >> 1;
+            m_lo = m_lo > a ? m_lo : a;
+            m_hi = m_hi < b ? m_hi : b;
+        }
+        const int cnt = m_hi - m_lo + 1;
+        for (int i = threadIdx.x; i < cnt * E; i += 256) {
+            const int m = m_lo + i / E, e = i - (i / E) * E;
+            const bool out_b = 2 * m - 1 < wn.x || 2 * m - 1 > wn.y, out_a = 2 * m < wn.x || 2 * m > wn.y;
+            // a half step outside the window is not stored: its propagator is Midle
+            const double2* Mb = out_b ? p.Midle + (size_t)si * N2 * N2
+                                      : p.M + ((size_t)si * 2 * p.n_steps + 2 * (m - 1) + 1) * N2 * N2;
+            double2 acc = c_zero();
+            if (e < N2 * N2) {
+                if (m >= p.n_steps) continue;
+                if (out_b && out_a) continue;  // F(m) is Fidle: not stored
+                const double2* Ma = out_a ? p.Midle + (size_t)si * N2 * N2
+                                          : p.M + ((size_t)si * 2 * p.n_steps + 2 * m) * N2 * N2;
+                const int r = e / N2, c = e - (e / N2) * N2;
+#pragma unroll
+                for (int k = 0; k < N2; ++k) c_fma(acc, Ma[r * N2 + k], Mb[k * N2 + c]);
+                p.F[((size_t)si * p.n_steps + m) * N2 * N2 + e] = acc;
+            } else {
+                if (out_b) continue;  // W(m) is Widle: not stored
+                const int q = e - N2 * N2, k = q / N2, a = q - (q / N2) * N2;
+#pragma unroll
+                for (int b = 0; b < N2; ++b) c_fma(acc, p.ovec[k * N2 + b], Mb[b * N2 + a]);
+                p.W[((size_t)si * (p.n_steps + 1) + m) * p.n_out * N2 + q] = acc;
+            }
+        }
+    }
+}
+
+// the idle operators of every system, with the fuse kernels' arithmetic (same summation order): Fidle = Midle Midle,
+// Widle = ovec . Midle — so a step outside the window reads the bits a stored copy would have held
+template <int N2>
+__global__ __launch_bounds__(256) void fuse_idle_kernel(FuseParams p) {
+    const int E = N2 * N2 + p.n_out * N2;
+    const long long total = (long long)p.n_sys * E;
     for (long long idx = (long long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
-        const long long blk = idx / E;
-        const int e = (int)(idx - blk * E);
-        const int si = (int)(blk / p.n_steps), m = (int)(blk - (long long)si * p.n_steps) + 1;
-        const double2* Mb = p.M + ((size_t)si * 2 * p.n_steps + 2 * (m - 1) + 1) * N2 * N2;
+        const int si = (int)(idx / E), e = (int)(idx - (long long)si * E);
+        const double2* Mi = p.Midle + (size_t)si * N2 * N2;
         double2 acc = c_zero();
         if (e < N2 * N2) {
-            if (m >= p.n_steps) continue;
-            const double2* Ma = p.M + ((size_t)si * 2 * p.n_steps + 2 * m) * N2 * N2;
             const int r = e / N2, c = e - (e / N2) * N2;
 #pragma unroll
-            for (int k = 0; k < N2; ++k) c_fma(acc, Ma[r * N2 + k], Mb[k * N2 + c]);
-            p.F[((size_t)si * p.n_steps + m) * N2 * N2 + e] = acc;
+            for (int k = 0; k < N2; ++k) c_fma(acc, Mi[r * N2 + k], Mi[k * N2 + c]);
+            p.Fidle[(size_t)si * N2 * N2 + e] = acc;
         } else {
             const int q = e - N2 * N2, k = q / N2, a = q - (q / N2) * N2;
 #pragma unroll
-            for (int b = 0; b < N2; ++b) c_fma(acc, p.ovec[k * N2 + b], Mb[b * N2 + a]);
-            p.W[((size_t)si * (p.n_steps + 1) + m) * p.n_out * N2 + q] = acc;
+            for (int b = 0; b < N2; ++b) c_fma(acc, p.ovec[k * N2 + b], Mi[b * N2 + a]);
+            p.Widle[(size_t)si * p.n_out * N2 + q] = acc;
         }
     }
 }
@@ -364,11 +500,16 @@ template <int N2>
 hipError_t launch_fs(const FuseParams& p, hipStream_t s) {
     const long long nblk = (long long)p.n_sys * p.n_steps;
     if (nblk <= 0) return hipSuccess;
-    if constexpr (N2 <= 9) {
-        const long long total = nblk * (N2 * N2 + p.n_out * N2);
-        hipLaunchKernelGGL(fuse_steps_flat_kernel<N2>, dim3((unsigned)std::min<long long>((total + 255) / 256,
-                                                                                          FP_MAX_BLOCKS)),
+    if (p.win) {
+        const long long total = (long long)p.n_sys * (N2 * N2 + p.n_out * N2);
+        hipLaunchKernelGGL(fuse_idle_kernel<N2>, dim3((unsigned)std::min<long long>((total + 255) / 256, FP_MAX_BLOCKS)),
                            dim3(256), 0, s, p);
+        if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+    }
+    if constexpr (N2 <= 9) {
+        const long long nb = (long long)p.n_sys * ((p.n_steps + FS_CHUNK - 1) / FS_CHUNK);
+        hipLaunchKernelGGL(fuse_steps_flat_kernel<N2>, dim3((unsigned)std::min<long long>(nb, FP_MAX_BLOCKS)), dim3(256),
+                           0, s, p);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(fuse_steps_kernel<N2>, dim3((unsigned)std::min<long long>(nblk, FP_MAX_BLOCKS)), dim3(256), 0,
@@ -391,10 +532,13 @@ hipError_t launch_fuse_steps(int N2, const FuseParams& p, hipStream_t s) {
 
 static hipError_t launch_free_prop_pass(int N2, const FreePropParams& p, hipStream_t s) {
     if (N2 == 4 && p.packed4) {  // packed4 = 0 (PQD_FP4=0 at plan creation): the general kernel (A/B)
-        const long long n_mat = p.idle_pass ? (long long)p.n_sys : (long long)p.n_sys * 2 * p.n_steps;
-        if (n_mat <= 0) return hipSuccess;
-        hipLaunchKernelGGL(free_prop4_kernel, dim3((unsigned)std::min<long long>((n_mat + 15) / 16, FP_MAX_BLOCKS)),
-                           dim3(256), 0, s, p);
+        FreePropParams q = p;
+        q.chunk = fp4_chunk(p);
+        const long long nblk = p.idle_pass ? ((long long)p.n_sys + 15) / 16
+                                           : (long long)p.n_sys * ((2LL * p.n_steps + q.chunk - 1) / q.chunk);
+        if (nblk <= 0) return hipSuccess;
+        hipLaunchKernelGGL(free_prop4_kernel, dim3((unsigned)std::min<long long>(nblk, FP_MAX_BLOCKS)), dim3(256), 0, s,
+                           q);
         return hipGetLastError();
     }
     switch (N2) {
@@ -407,7 +551,8 @@ static hipError_t launch_free_prop_pass(int N2, const FreePropParams& p, hipStre
     }
 }
 
-// with p.Midle: the idle propagators first (one per system), then every half step (idle ones copy Midle)
+// with p.Midle: the idle propagators first (one per system), then (with p.win) the pulse windows, then every half step
+// inside its window (idle ones copy Midle)
 hipError_t launch_free_prop(int N2, const FreePropParams& p, hipStream_t s) {
     FreePropParams q = p;
     if (p.Midle && p.n_steps > 0) {
@@ -416,5 +561,13 @@ hipError_t launch_free_prop(int N2, const FreePropParams& p, hipStream_t s) {
         if (e != hipSuccess) return e;
     }
     q.idle_pass = 0;
+    if (!p.Midle) q.win = nullptr;  // windows need the idle propagator
+    if (q.win && p.n_steps > 0) {
+        hipLaunchKernelGGL(free_win_init_kernel, dim3((p.n_sys + 255) / 256), dim3(256), 0, s, q.win, p.n_sys);
+        const long long nblk = (long long)p.n_sys * ((2LL * p.n_steps + 255) / 256);
+        hipLaunchKernelGGL(free_win_kernel, dim3((unsigned)std::min<long long>(nblk, FP_MAX_BLOCKS)), dim3(256), 0, s,
+                           q);
+        if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+    }
     return launch_free_prop_pass(N2, q, s);
 }

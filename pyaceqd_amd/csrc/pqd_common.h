@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <climits>
 
 #define PQD_WAVE 64
 
@@ -49,6 +50,9 @@ struct FreePropParams {
     double2* Midle;          // n_sys*N2*N2: exp(L0 w)^n_sub, the propagator of a half step whose pulse samples are all
                              //   exactly zero (built first, copied for every such half step); NULL: always compute
     int idle_pass;           // 1: this launch builds Midle (one matrix per system, samples taken as 0)
+    int2* win;               // n_sys pulse windows (lo, hi): every half step h < lo or h > hi is idle and is NOT stored
+                             //   (readers take Midle, see fw_M); NULL: every half step stored (copies of Midle)
+    int chunk;               // free_prop4_kernel: half steps per workgroup (set by its launcher)
 };
 
 struct SweepParams {
@@ -100,7 +104,32 @@ struct SweepParams {
     unsigned spin_limit;     // split groups: polls before a wait for the peers times out (PQD_SPLIT_SPIN, tests)
     int n_steps;             // grid steps (operand prefetch bound)
     int n_blk;               // blocks of the launch (quad kernel: quads; tail workgroups check it)
+    const int2* win;         // per-system pulse windows (FreePropParams::win) or NULL; outside them M, F, W are the
+    const double2* Midle;    //   system's idle operators: Midle [n_sys][N2 x N2], Fidle = Midle Midle [n_sys][N2 x N2],
+    const double2* Fidle;    //   Widle = ovec . Midle [n_sys][n_out][N2]
+    const double2* Widle;
 };
+
+// ---- free propagators through the pulse windows: M(h), F(n) = M(2n) M(2n-1) and W(n) = ovec . M(2n-1) of system sys
+// are stored only where the half steps involved lie inside the system's window [lo, hi]; outside, the propagator is
+// the idle one (the same bits the builder copied there before windows: Midle, and Fidle / Widle computed from it by
+// the fuse kernels' own arithmetic)
+__device__ __forceinline__ int2 fw_win(const SweepParams& p, int sys) {
+    return p.win ? p.win[sys] : make_int2(INT_MIN, INT_MAX);
+}
+__device__ __forceinline__ bool fw_out(int2 w, int h) { return h < w.x || h > w.y; }
+__device__ __forceinline__ const double2* fw_M(const SweepParams& p, int sys, int2 w, int h, int m2) {
+    return fw_out(w, h) ? p.Midle + (size_t)sys * m2 : p.M + (size_t)sys * p.m_stride + (size_t)h * m2;
+}
+__device__ __forceinline__ const double2* fw_F(const SweepParams& p, int sys, int2 w, int n, int m2) {
+    return (fw_out(w, 2 * n - 1) && fw_out(w, 2 * n)) ? p.Fidle + (size_t)sys * m2
+                                                      : p.F + (size_t)sys * p.f_stride + (size_t)n * m2;
+}
+// the n_out rows of W(n) (n_out * N2 elements)
+__device__ __forceinline__ const double2* fw_W(const SweepParams& p, int sys, int2 w, int n, int N2) {
+    return fw_out(w, 2 * n - 1) ? p.Widle + (size_t)sys * p.n_out * N2
+                                : p.W + (size_t)sys * p.w_stride + (size_t)n * p.n_out * N2;
+}
 
 
 
@@ -143,6 +172,10 @@ struct FuseParams {          // F(m) = M_a(m) M_b(m-1) (1 <= m < n_steps), W(m) 
     double2* W;
     const double2* ovec;
     int n_sys, n_steps, n_out;
+    const int2* win;         // FreePropParams::win or NULL: F(m) / W(m) whose half steps are all outside are not stored
+    const double2* Midle;    // with win: the idle pass writes Fidle = Midle Midle and Widle = ovec . Midle per system
+    double2* Fidle;
+    double2* Widle;
 };
 
 hipError_t launch_free_prop(int N2, const FreePropParams& p, hipStream_t s);

@@ -213,6 +213,8 @@ struct pqd_plan {
     DevBuf<double2> Xs;
     DevBuf<unsigned> cnt, err;
     DevBuf<double2> L0, S, T, samples, M, Midle, F, W, rho0, ovec, sop, out;
+    DevBuf<double2> Fidle, Widle;  // idle fused operators per system (pulse windows)
+    DevBuf<int2> win;              // per-system pulse windows (free_prop.hip free_win_kernel), PQD_WIN=0: none
     DevBuf<FreePropSys> systab;
     FuseParams fu{};
     DevBuf<int> sched, blk_traj, blk_end, blk_sys, blk_act, blk_src, traj_sys, wbeg, wend, ev_start;
@@ -853,6 +855,12 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     if (const char* ie = getenv("PQD_IDLE"); !(ie && atoi(ie) == 0)) {  // PQD_IDLE=0: compute every half step (A/B)
         HIPCHK(P->Midle.alloc((size_t)n_sys * m2));
         P->fp.Midle = P->Midle.p;
+        // pulse windows: half steps outside a system's [first, last] non-idle half step are neither stored nor
+        // re-read (sweeps take Midle / Fidle / Widle there); PQD_WIN=0 stores every half step (A/B)
+        if (const char* we = getenv("PQD_WIN"); !(we && atoi(we) == 0)) {
+            HIPCHK(P->win.alloc((size_t)n_sys));
+            P->fp.win = P->win.p;
+        }
     }
     P->fp.ta = grid->ta; P->fp.dt = grid->dt; P->fp.n_steps = ns; P->fp.n_sub = grid->n_sub; P->fp.M = P->M.p;
 
@@ -893,10 +901,16 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
         HIPCHK(P->F.alloc((size_t)n_sys * ns * m2));
         HIPCHK(P->W.alloc((size_t)n_sys * (ns + 1) * n_out * N2));
         P->fu = FuseParams{P->M.p, P->F.p, P->W.p, P->ovec.p, n_sys, ns, n_out};
+        if (P->win.p) {
+            HIPCHK(P->Fidle.alloc((size_t)n_sys * m2));
+            HIPCHK(P->Widle.alloc((size_t)n_sys * n_out * N2));
+            P->fu.win = P->win.p; P->fu.Midle = P->Midle.p; P->fu.Fidle = P->Fidle.p; P->fu.Widle = P->Widle.p;
+        }
         sp.f_stride = (long long)ns * m2;
         sp.w_stride = (long long)(ns + 1) * n_out * N2;
     }
     sp.F = P->F.p; sp.W = P->W.p;
+    sp.win = P->win.p; sp.Midle = P->Midle.p; sp.Fidle = P->Fidle.p; sp.Widle = P->Widle.p;
     sp.woff = P->woff.p; sp.ev_start = P->ev_start.p; sp.ev = P->ev.p; sp.sop = P->sop.p; sp.out = P->out.p;
     sp.n_steps = ns;
     sp.n_blk = nb;

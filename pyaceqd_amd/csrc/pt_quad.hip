@@ -101,7 +101,7 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : 1) voi
     const int sys = traj >= 0 ? p.traj_sys[traj] : 0;
     int ev_cur = traj >= 0 ? p.ev_start[traj] : 0;
     const int ev_lim = traj >= 0 ? p.ev_start[traj + 1] : 0;
-    const double2* Mg = p.M + (size_t)sys * p.m_stride;
+    const int2 wq = fw_win(p, sys);  // pulse window: M, F outside it are the system's idle operators (fw_M, fw_F)
     const int opi = lc * 4 + la;  // this lane's operator element Op[alpha' = lc][alpha = la]
     // ---- T-layout (l = 16 t + 4 k + alpha): the traces, four lanes per (trajectory, output k < 4), reduced over alpha
     // by DPP inside the quad of lanes
@@ -111,6 +111,7 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : 1) voi
     const int wb2 = traj2 >= 0 ? p.wbeg[traj2] : INT_MAX, we2 = traj2 >= 0 ? p.wend[traj2] : -1;
     const long long wo2 = traj2 >= 0 ? p.woff[traj2] : 0;
     const int sys2 = traj2 >= 0 ? p.traj_sys[traj2] : 0;
+    const int2 wq2 = fw_win(p, sys2);
     const int k2c = k2 < NO ? k2 : NO - 1;
 
     // ---- loop bounds: the quad's [first activation, last output], the workgroup's hull (barriers are workgroup-wide)
@@ -189,15 +190,21 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : 1) voi
 #pragma unroll
         for (int cg = 0; cg < NCG; ++cg) cl[cg] = cv[CW * h + 4 * cg + lc];
     };
-    const double2* Fp = fuse ? p.F + (size_t)sys * p.f_stride : p.M;  // unfused plans: the ring reads p.M[0]
-    const double2* Wp = fuse ? p.W + (size_t)sys2 * p.w_stride : p.M;
+    // unfused plans: the ring reads p.M[0] (unused); the window selects are selects, not branches (the ring loads
+    // stay unconditional)
     const size_t fmul = fuse ? 1 : 0;
-    auto ldF = [&](int n) { return Fp[fmul * ((size_t)(n < ns ? n : ns - 1) * 16 + opi)]; };
+    auto ldF = [&](int n) {
+        const double2* f = fuse ? fw_F(p, sys, wq, n < ns ? n : ns - 1, 16) : p.M;
+        return f[fmul * opi];
+    };
     auto ldS = [&](int n) { return p.sched[n < ns ? n : ns - 1]; };
     const double2 ov = p.ovec[k2c * 4 + a2];  // T-layout: element (k2, a2) of the output rows (unfused steps)
     double2 fpre[2], wv[2];
     int sr[2];
-    auto ldW = [&](int j, int n) { wv[j] = Wp[fmul * (((size_t)(n <= ns ? n : ns) * NO + k2c) * 4 + a2)]; };
+    auto ldW = [&](int j, int n) {
+        const double2* w = fuse ? fw_W(p, sys2, wq2, n <= ns ? n : ns, 4) : p.M;
+        wv[j] = w[fmul * ((size_t)k2c * 4 + a2)];
+    };
     const int n0 = n_lo;
     int q_cur = __builtin_amdgcn_readfirstlane(ldS(n0));
     int c_cur = n0 == 0 ? -1 : __builtin_amdgcn_readfirstlane(ldS(n0 - 1));
@@ -285,14 +292,14 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : 1) voi
                     const bool mine = k0 < 9;
                     double2 a = c_zero();
                     if (k0 == 0) { a = fpre[S]; k0 = 9; }
-                    else if (k0 == 1) { a = Mg[(size_t)(2 * n - 1) * 16 + opi]; k0 = 2; }
+                    else if (k0 == 1) { a = fw_M(p, sys, wq, 2 * n - 1, 16)[opi]; k0 = 2; }
                     else if (k0 == 2) {
                         if (evn.x == n && evn.y == 1) {
                             a = p.sop[(size_t)evn.z * 16 + opi];
                             ++ev_cur;
                             evn = ev_cur < ev_lim ? p.ev[ev_cur] : make_int4(INT_MAX, 0, 0, 0);
                         } else {
-                            a = Mg[(size_t)(2 * n) * 16 + opi];
+                            a = fw_M(p, sys, wq, 2 * n, 16)[opi];
                             k0 = 9;
                         }
                     }
@@ -318,7 +325,7 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : 1) voi
             if (a2 == 0 && win2 && k2 < NO) p.out[wo2 + (long long)(n - wb2) * NO + k2] = x;
             for (int kb = 4; kb < NO; kb += 4) {  // more than four outputs: further passes, rows loaded here
                 const int k = kb + k2 < NO ? kb + k2 : NO - 1;
-                const double2 w = f2 ? p.W[(size_t)sys2 * p.w_stride + ((size_t)n * NO + k) * 4 + a2] : p.ovec[k * 4 + a2];
+                const double2 w = f2 ? fw_W(p, sys2, wq2, n, 4)[k * 4 + a2] : p.ovec[k * 4 + a2];
                 const double2 y = quad_sum(c_mul(w, r));
                 if (a2 == 0 && win2 && kb + k2 < NO) p.out[wo2 + (long long)(n - wb2) * NO + kb + k2] = y;
             }
@@ -381,7 +388,7 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : 1) voi
             while (__ballot(k0 < 9)) {
                 bool mine = k0 < 9;
                 double2 a = c_zero();
-                if (k0 == 0) { a = Mg[(size_t)(2 * n + 1) * 16 + opi]; k0 = 1; }
+                if (k0 == 0) { a = fw_M(p, sys, wq, 2 * n + 1, 16)[opi]; k0 = 1; }
                 else if (k0 == 1) {
                     if (evn.x == n + 1 && evn.y == 0) {
                         a = p.sop[(size_t)evn.z * 16 + opi];

@@ -91,9 +91,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
     const int wb = p.wbeg[t], we = p.wend[t];
     const long long wo = p.woff[t];
     const int sy = p.traj_sys[t];
-    const double2* __restrict__ Mg = p.M + (size_t)sy * p.m_stride;
-    const double2* __restrict__ Fg = p.F + (size_t)sy * p.f_stride;
-    const double2* __restrict__ Wg = p.W + (size_t)sy * p.w_stride;
+    const int2 wn = fw_win(p, sy);  // pulse window: M, F, W outside it are the system's idle operators
     double2* __restrict__ Xt = X + (size_t)t * 2 * E;
     // descriptor over this trajectory's two exchange slots, from workgroup-uniform values only
     const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(Xt, 0, 2 * E * 16, 0x00020000);
@@ -181,8 +179,8 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         int rb;  // row g of the state the PT contracts
         if (fz) {
             // only row g of F(n) Q is needed here; Q itself stays for the deferred output(n) through W(n)
-            if (n >= n_end) { output(n, Wg + (size_t)n * p.n_out * N2); break; }
-            if (tid < N2) smem[OPO + tid] = pre ? frow : gld(Fg + (size_t)n * m2 + (size_t)g * N2 + tid);
+            if (n >= n_end) { output(n, fw_W(p, sy, wn, n, N2)); break; }
+            if (tid < N2) smem[OPO + tid] = pre ? frow : gld(fw_F(p, sy, wn, n, m2) + (size_t)g * N2 + tid);
             __syncthreads();
             if (tid < CHI) {
                 double2 acc = c_zero();
@@ -193,7 +191,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
             __syncthreads();
             rb = to + g * CHI;
         } else {
-            if (n > 0) apply_global(Mg + (size_t)(2 * (n - 1) + 1) * m2);
+            if (n > 0) apply_global(fw_M(p, sy, wn, 2 * (n - 1) + 1, m2));
             while (ev_cur < ev_lim) {  // applyBefore MTOs at n
                 const int4 ev = p.ev[ev_cur];
                 if (ev.x != n || ev.y != 0) break;
@@ -208,7 +206,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
                 apply_global(p.sop + (size_t)ev.z * m2);
                 ++ev_cur;
             }
-            apply_global(Mg + (size_t)(2 * n) * m2);
+            apply_global(fw_M(p, sy, wn, 2 * n, m2));
             rb = qo + g * CHI;
         }
         // ---- PT row g: y = row . S(n) -> exchange buffer (parity n & 1)
@@ -229,10 +227,10 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) __hip_atomic_fetch_add((gu32*)ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (fz) output(n, Wg + (size_t)n * p.n_out * N2);  // off the group's critical path (workgroup 0 only)
+        if (fz) output(n, fw_W(p, sy, wn, n, N2));  // off the group's critical path (workgroup 0 only)
         if (n + 1 < n_end) fetch_slice(n + 1);
         pre = p.fuse && n + 1 < n_end && !has_event(n + 1);
-        if (pre && tid < N2) frow = gld(Fg + (size_t)(n + 1) * m2 + (size_t)g * N2 + tid);
+        if (pre && tid < N2) frow = gld(fw_F(p, sy, wn, n + 1, m2) + (size_t)g * N2 + tid);
         if (tid < 64) {
             const unsigned target = (unsigned)G * (unsigned)(n + 1);
             unsigned spins = 0;
