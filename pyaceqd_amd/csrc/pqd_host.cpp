@@ -728,6 +728,9 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     {
         const char* e = getenv("PQD_QUAD");
         P->quad = pt && !P->split && quad_supported(N2, P->CHI) && !(e && atoi(e) == 0);
+        // chi = 32: one quad per workgroup, so the two 8-column-strip workgroups sharing a CU barrier independently
+        // (C2: 19.8 -> 18.4 ms per launch with the strips below, profiles/r02/quad/envab_qpw_qcg.log)
+        if (P->CHI == 32) P->qpw = 1;
         if (const char* w = getenv("PQD_QPW")) P->qpw = std::max(1, atoi(w));
         if (P->quad) BT = 4;
     }
@@ -799,7 +802,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
         // blocks resident at once: quads (one workgroup of qpw quads per CU) or BT-workgroups as the LDS allows
         int64_t conc = n_cu;
         if (P->quad) {
-            conc = (int64_t)n_cu * std::max(1, P->qpw);
+            conc = (int64_t)n_cu * (P->CHI == 32 ? 2 : std::max(1, P->qpw));  // chi = 32: two quads per CU either way
         } else {
             const int64_t lds = ((int64_t)BT * (N2 * (P->CHI + 1) + 4) + (int64_t)BT * N2) * 16;
             conc = (int64_t)n_cu * std::max<int64_t>(1, std::min<int64_t>(4, (160 * 1024) / std::max<int64_t>(1, lds)));
@@ -914,11 +917,11 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     sp.woff = P->woff.p; sp.ev_start = P->ev_start.p; sp.ev = P->ev.p; sp.sop = P->sop.p; sp.out = P->out.p;
     sp.n_steps = ns;
     sp.n_blk = nb;
-    // quad kernel: with no more quads than CUs the step latency sets the time, and strips of 8 columns (twice the
-    // waves, two per SIMD) overlap one wave's round trips with the other's MFMAs (C2 single run 17.2 -> 13.1 ms);
-    // a full device runs the 16-column strips (measured equal on the 2,048-trajectory scan)
+    // quad kernel: strips of 8 columns (twice the waves, two per SIMD) overlap one wave's round trips with the
+    // other's MFMAs: with no more quads than CUs (C2 single run 17.2 -> 13.1 ms), and at chi = 32 with one quad per
+    // workgroup on a full device too (C2 scan 18.9 -> 18.4 ms); chi = 16 full devices keep the 16-column strips
     if (P->quad) {
-        P->qcg = nb <= n_cu ? 2 : 4;
+        P->qcg = (nb <= n_cu || (P->CHI == 32 && P->qpw == 1)) ? 2 : 4;
         if (const char* e = getenv("PQD_QCG")) P->qcg = atoi(e) == 2 ? 2 : 4;
     }
     finalize_trunks(P);

@@ -71,7 +71,7 @@ __device__ __forceinline__ double2 quad_sum(double2 v) {  // sum over lanes l ^ 
     return v;
 }
 
-// NCG = 4-column groups per wave: 4 (strips of 16 columns, one wave per SIMD) or 2 (strips of 8, twice the waves,
+// NCG = 4-column groups per wave: 4 (strips of 16 columns, one wave per SIMD), 2 (strips of 8, twice the waves,
 // two per SIMD so one wave's LDS round trips and barrier hide behind the other's MFMAs)
 template <int CHI, int QPW, bool STAMP = false, int NCG = 4>
 __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : 1) void pt_quad_kernel(SweepParams p) {
