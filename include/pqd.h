@@ -127,6 +127,16 @@ int pqd_propagate_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems, 
                         int32_t n_out, const pqd_c128* out_ops, const pqd_traj* traj, pqd_c128* out,
                         int64_t out_len);
 
+/* pqd_propagate_multi returning ACE's output table instead of the flat output buffer: per trajectory t, at offset
+ * sum_{u<t} (1 + n_out) * L_u (L = out_end - out_begin + 1), (1 + n_out) rows of L values, row 0 = the times
+ * ta + dt * step (imaginary part 0), row 1 + k = output k. Replaces reading the ACE outfile
+ * (general_system.py:343: `np.loadtxt(outfile, dtype=complex).T`, one table per ACE run); the transposition runs on
+ * the device, so a caller gets every trajectory's table as a view of one buffer. table_len >= sum of the tables. */
+int pqd_propagate_table(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems, const int32_t* traj_sys,
+                        const pqd_grid* grid, const pqd_pt* pt, const int32_t* sched, const pqd_c128* rho0,
+                        int32_t n_out, const pqd_c128* out_ops, const pqd_traj* traj, pqd_c128* table,
+                        int64_t table_len);
+
 /* device-resident plan for repeated execution (bench, scans): same arguments as pqd_propagate(_multi). */
 int pqd_plan_create(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* grid, const pqd_pt* pt,
                     const int32_t* sched, const pqd_c128* rho0, int32_t n_out, const pqd_c128* out_ops,
@@ -150,6 +160,9 @@ int pqd_plan_download(pqd_plan* plan, pqd_c128* out, int64_t out_len);
  * out_len complex values, e.g. a torch tensor that a collective then gathers over xGMI (scan.py). Replaces the
  * reference's result lists assembled from per-process CSV files (correlations.py:171-183). */
 int pqd_plan_copy_output(pqd_plan* plan, void* dst, int64_t out_len);
+/* the plan's ACE-table length (complex values, layout of pqd_propagate_table) and pqd_plan_synchronize + the tables */
+int pqd_plan_table_len(const pqd_plan* plan, int64_t* table_len);
+int pqd_plan_download_table(pqd_plan* plan, pqd_c128* table, int64_t table_len);
 #define PQD_PATH_NOPT 0     /* no PT: one wave per trajectory */
 #define PQD_PATH_BATCHED 1  /* lock-step PT sweep, bt trajectories per workgroup */
 #define PQD_PATH_SPLIT 2    /* one trajectory over N^2 workgroups (latency path) */

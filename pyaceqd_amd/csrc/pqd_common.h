@@ -182,6 +182,9 @@ hipError_t launch_free_prop(int N2, const FreePropParams& p, hipStream_t s);
 // flags |= 1 if any of the n complex values is NaN or Inf (one pass over the output buffer at synchronize: the sweep
 // kernels carry no per-store check, which cost 1.7% of the headline kernel)
 hipError_t launch_check_finite(const double2* v, int64_t n, unsigned* flags, hipStream_t s);
+hipError_t launch_table(const double2* out, const long long* woff, const int* wbeg, const int* wend,
+                        const long long* toff, int n_traj, int n_out, double t_start, double dt, double2* table,
+                        hipStream_t s);
 hipError_t launch_fuse_steps(int N2, const FuseParams& p, hipStream_t s);
 // waves per trajectory in the PT sweep: a 4-trajectory workgroup (N2 > 16 or chi = 128) runs 8 waves, two per
 // trajectory (each owns half of the bond columns in the column phases), so every SIMD holds two waves

@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 using cd = std::complex<double>;
@@ -110,21 +111,6 @@ void dissipator(int N, const cd* Lk, double g, cd* S) {  // S += g (L . L^dag - 
                     S[(size_t)(i * N + j) * N2 + (k * N + l)] += g * Lk[i * N + k] * std::conj(Lk[j * N + l]);
     kron_left(N, LdL.data(), S, cd(-0.5 * g));
     kron_right(N, LdL.data(), S, cd(-0.5 * g));
-}
-void mto_superop(int N, int kind, const cd* A, cd* S) {
-    const int N2 = N * N;
-    std::fill(S, S + (size_t)N2 * N2, cd(0));
-    if (kind == 1) {
-        kron_left(N, A, S, 1.0);
-    } else if (kind == 2) {
-        kron_right(N, A, S, 1.0);
-    } else {  // A rho A^dag: A (x) conj(A)
-        for (int i = 0; i < N; ++i)
-            for (int j = 0; j < N; ++j)
-                for (int k = 0; k < N; ++k)
-                    for (int l = 0; l < N; ++l)
-                        S[(size_t)(i * N + j) * N2 + (k * N + l)] = A[i * N + k] * std::conj(A[j * N + l]);
-    }
 }
 void matmul_sq(int n, const cd* A, const cd* B, cd* Cm) {
     std::vector<cd> t((size_t)n * n, 0.0);
@@ -236,6 +222,11 @@ struct pqd_plan {
     FreePropParams fp{};
     SweepParams sp{};
     int64_t out_len = 0;
+    int n_out = 0;
+    double t_start = 0.0, dt = 0.0;
+    std::vector<long long> toff;  // ACE-table offsets per trajectory ((1 + n_out) rows of its window), + total
+    DevBuf<long long> toff_d;
+    DevBuf<double2> table;
     DevBuf<unsigned> flags;       // bit 0: non-finite output (PQD_ERR_NUMERIC)
     int split_fallbacks = 0;      // split launches that timed out and were re-run on the batched kernel
     // hipEvent triplets (start, free propagators done, sweep done) of the last RING executes, created once
@@ -627,6 +618,10 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     auto* P = new pqd_plan;
     std::unique_ptr<pqd_plan> guard(P);
     P->ctx = ctx; P->N2 = N2; P->n_traj = tr->n_traj; P->n_steps = ns; P->out_len = out_len;
+    P->n_out = n_out; P->t_start = grid->ta; P->dt = grid->dt;
+    P->toff.assign(tr->n_traj + 1, 0);
+    for (int t = 0; t < tr->n_traj; ++t)
+        P->toff[t + 1] = P->toff[t] + (long long)(1 + n_out) * (tr->out_end[t] - tr->out_begin[t] + 1);
     P->nopt = (pt == nullptr);
     P->CHI = pt ? pt->CHI : 1;
     P->n_sys = n_sys;
@@ -638,13 +633,19 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     for (int t = 0; t < tr->n_traj; ++t) tsys[t] = traj_sys ? traj_sys[t] : 0;
     HIPCHK(P->traj_sys.upload(tsys.data(), tsys.size(), s));
 
-    // ---- MTO events: per trajectory, stable-sorted by (step, phase), same-slot ops composed
+    // ---- MTO events: per trajectory, stable-sorted by (step, phase), same-slot ops composed. Every MTO kind is
+    // rho -> L rho R ("": A rho A^dag, _left: A rho, _right: rho A), so a slot's ops compose as N x N products
+    // (L = L_k ... L_1, R = R_1 ... R_k) and its superoperator is L (x) R^T; identical (L, R) pairs share one
+    // superoperator (a two-time sweep applies the same operators at every t1).
     std::vector<std::vector<int>> per(tr->n_traj);
     for (int q = 0; q < tr->n_mto; ++q) per[tr->mto_traj[q]].push_back(q);
     std::vector<int> ev_start(tr->n_traj + 1, 0);
     std::vector<int4> evs;
     std::vector<cd> sops;
-    std::vector<cd> tmpS(m2), acc(m2);
+    std::unordered_map<std::string, int> sop_index;
+    const size_t nn = (size_t)N * N;
+    std::vector<cd> Lm(nn), Rm(nn), Lq(nn), Rq(nn), key_buf(2 * nn);
+    auto eye = [&](std::vector<cd>& M) { std::fill(M.begin(), M.end(), cd(0)); for (int i = 0; i < N; ++i) M[(size_t)i * N + i] = 1.0; };
     for (int t = 0; t < tr->n_traj; ++t) {
         auto& v = per[t];
         auto key = [&](int q) { return 2 * tr->mto_step[q] + (tr->mto_before[q] ? 0 : 1); };
@@ -653,15 +654,39 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
         size_t i = 0;
         while (i < v.size()) {
             const int k0 = key(v[i]);
-            bool first = true;
+            eye(Lm);
+            eye(Rm);
             for (; i < v.size() && key(v[i]) == k0; ++i) {
                 const int q = v[i];
-                mto_superop(N, tr->mto_kind[q], C(tr->mto_ops) + (size_t)q * N * N, tmpS.data());
-                if (first) { acc = tmpS; first = false; }
-                else matmul_sq(N2, tmpS.data(), acc.data(), acc.data());
+                const cd* A = C(tr->mto_ops) + (size_t)q * nn;
+                const int kind = tr->mto_kind[q];
+                if (kind == 2) eye(Lq); else std::copy(A, A + nn, Lq.begin());
+                if (kind == 1) eye(Rq);
+                else if (kind == 2) std::copy(A, A + nn, Rq.begin());
+                else
+                    for (int r = 0; r < N; ++r)
+                        for (int c = 0; c < N; ++c) Rq[(size_t)r * N + c] = std::conj(A[(size_t)c * N + r]);
+                matmul_sq(N, Lq.data(), Lm.data(), Lm.data());  // L <- L_q L
+                matmul_sq(N, Rm.data(), Rq.data(), Rm.data());  // R <- R R_q
             }
-            const int idx = (int)(sops.size() / m2);
-            sops.insert(sops.end(), acc.begin(), acc.end());
+            std::copy(Lm.begin(), Lm.end(), key_buf.begin());
+            std::copy(Rm.begin(), Rm.end(), key_buf.begin() + nn);
+            std::string kb(reinterpret_cast<const char*>(key_buf.data()), key_buf.size() * sizeof(cd));
+            auto it = sop_index.find(kb);
+            int idx;
+            if (it != sop_index.end()) {
+                idx = it->second;
+            } else {
+                idx = (int)(sops.size() / m2);
+                sop_index.emplace(std::move(kb), idx);
+                sops.resize(sops.size() + m2);
+                cd* S = sops.data() + (size_t)idx * m2;
+                for (int a = 0; a < N; ++a)
+                    for (int j = 0; j < N; ++j)
+                        for (int k = 0; k < N; ++k)
+                            for (int l = 0; l < N; ++l)
+                                S[(size_t)(a * N + j) * N2 + (k * N + l)] = Lm[(size_t)a * N + k] * Rm[(size_t)l * N + j];
+            }
             evs.push_back(make_int4(k0 >> 1, k0 & 1, idx, 0));
         }
     }
@@ -1024,6 +1049,30 @@ int pqd_plan_download(pqd_plan* P, pqd_c128* out, int64_t out_len) {
     return rc;  // PQD_ERR_NUMERIC still hands the values over (they show where the run went bad)
 }
 
+int pqd_plan_table_len(const pqd_plan* P, int64_t* table_len) {
+    if (!P || !table_len) return fail(PQD_ERR_ARG, "NULL argument");
+    *table_len = P->toff.empty() ? 0 : P->toff.back();
+    return PQD_OK;
+}
+
+int pqd_plan_download_table(pqd_plan* P, pqd_c128* table, int64_t table_len) {
+    if (!P || !table) return fail(PQD_ERR_ARG, "NULL argument");
+    const long long need = P->toff.empty() ? 0 : P->toff.back();
+    if (table_len < need) return fail(PQD_ERR_ARG, "table_len %lld < %lld", (long long)table_len, need);
+    int rc = pqd_plan_synchronize(P);
+    if (rc && rc != PQD_ERR_NUMERIC) return rc;
+    if (need > 0) {
+        hipStream_t s = P->ctx->stream;
+        if (!P->toff_d.p) HIPCHK(P->toff_d.upload(P->toff.data(), P->toff.size(), s));
+        if (!P->table.p) HIPCHK(P->table.alloc((size_t)need));
+        HIPCHK(launch_table(P->out.p, P->woff.p, P->wbeg.p, P->wend.p, P->toff_d.p, P->n_traj, P->n_out, P->t_start,
+                            P->dt, P->table.p, s));
+        HIPCHK(hipMemcpyAsync(table, P->table.p, (size_t)need * sizeof(double2), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    return rc;
+}
+
 int pqd_plan_copy_output(pqd_plan* P, void* dst, int64_t out_len) {
     if (!P || !dst) return fail(PQD_ERR_ARG, "NULL argument");
     if (out_len < P->out_len) return fail(PQD_ERR_ARG, "out_len %lld < plan out_len %lld", (long long)out_len, (long long)P->out_len);
@@ -1088,6 +1137,24 @@ int pqd_propagate_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems, 
     if (rc) return rc;
     rc = pqd_plan_execute(P, 1);
     if (!rc) rc = pqd_plan_download(P, out, out_len);
+    pqd_plan_destroy(P);
+    return rc;
+}
+
+int pqd_propagate_table(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems, const int32_t* traj_sys,
+                        const pqd_grid* grid, const pqd_pt* pt, const int32_t* sched, const pqd_c128* rho0,
+                        int32_t n_out, const pqd_c128* out_ops, const pqd_traj* tr, pqd_c128* table,
+                        int64_t table_len) {
+    if (!tr) return fail(PQD_ERR_ARG, "NULL argument");
+    int64_t out_len = 0;
+    for (int t = 0; t < tr->n_traj; ++t)
+        out_len = std::max<int64_t>(out_len, tr->out_offset[t] + (int64_t)(tr->out_end[t] - tr->out_begin[t] + 1) * n_out);
+    pqd_plan* P = nullptr;
+    int rc = pqd_plan_create_multi(ctx, n_sys, systems, traj_sys, grid, pt, sched, rho0, n_out, out_ops, tr,
+                                   std::max<int64_t>(1, out_len), &P);
+    if (rc) return rc;
+    rc = pqd_plan_execute(P, 1);
+    if (!rc) rc = pqd_plan_download_table(P, table, table_len);
     pqd_plan_destroy(P);
     return rc;
 }

@@ -16,7 +16,35 @@ __global__ __launch_bounds__(256) void check_finite_kernel(const double2* __rest
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flags, 1u);
 }
 
+// ACE's output table per trajectory (general_system.py:343, `np.loadtxt(outfile).T`): row 0 the times
+// t_start + dt * step, rows 1 + k the outputs, for the steps of the trajectory's window. One workgroup per trajectory
+// (grid-stride), lanes over steps; the time is dt * step then + t_start in two roundings, as numpy forms it.
+__global__ __launch_bounds__(256) void table_kernel(const double2* __restrict__ out, const long long* __restrict__ woff,
+                                                    const int* __restrict__ wbeg, const int* __restrict__ wend,
+                                                    const long long* __restrict__ toff, int n_traj, int n_out,
+                                                    double t_start, double dt, double2* __restrict__ table) {
+    for (int t = blockIdx.x; t < n_traj; t += gridDim.x) {
+        const int b = wbeg[t], L = wend[t] - wbeg[t] + 1;
+        const double2* o = out + woff[t];
+        double2* tb = table + toff[t];
+        for (int i = threadIdx.x; i < L; i += 256) {
+#pragma clang fp contract(off)  // no FMA: the product rounds before the sum, as in numpy
+            tb[i] = make_double2(dt * (double)(b + i) + t_start, 0.0);
+            for (int k = 0; k < n_out; ++k) tb[(size_t)(1 + k) * L + i] = o[(size_t)i * n_out + k];
+        }
+    }
+}
+
 }  // namespace
+
+hipError_t launch_table(const double2* out, const long long* woff, const int* wbeg, const int* wend,
+                        const long long* toff, int n_traj, int n_out, double t_start, double dt, double2* table,
+                        hipStream_t s) {
+    if (n_traj <= 0) return hipSuccess;
+    hipLaunchKernelGGL(table_kernel, dim3((unsigned)std::min(n_traj, 1 << 16)), dim3(256), 0, s, out, woff, wbeg,
+                       wend, toff, n_traj, n_out, t_start, dt, table);
+    return hipGetLastError();
+}
 
 hipError_t launch_check_finite(const double2* v, int64_t n, unsigned* flags, hipStream_t s) {
     if (n <= 0) return hipSuccess;

@@ -253,6 +253,52 @@ def propagate(system, grid: Grid, rho0, out_ops: Sequence, traj: Trajectories,
     return split_output(out, traj, len(out_ops))
 
 
+def table_offsets(traj: Trajectories, n_out):
+    """offsets of the per-trajectory ACE tables ((1 + n_out) rows of the window) in a pqd_propagate_table buffer"""
+    L = np.asarray(traj.out_end, dtype=np.int64) - np.asarray(traj.out_begin, dtype=np.int64) + 1
+    off = np.zeros(traj.n_traj + 1, dtype=np.int64)
+    np.cumsum((1 + n_out) * L, out=off[1:])
+    return off, L
+
+
+def split_table(table, traj, n_out):
+    """flat table buffer -> list of (1 + n_out, window_len) views, one per trajectory"""
+    off, L = table_offsets(traj, n_out)
+    return [table[off[t]: off[t + 1]].reshape(1 + n_out, int(L[t])) for t in range(traj.n_traj)]
+
+
+def tables_from_outputs(outs, traj: Trajectories, grid: Grid):
+    """host form of the device table assembly (pqd_propagate_table): per-trajectory (window_len, n_out) outputs ->
+    (1 + n_out, window_len) tables with the step times in row 0 (the oracle-backed tests route through this)"""
+    res = []
+    for b, o in zip(traj.out_begin, outs):
+        r = np.empty((1 + o.shape[1], o.shape[0]), dtype=np.complex128)
+        r[0] = grid.ta + grid.dt * np.arange(int(b), int(b) + o.shape[0])
+        r[1:] = o.T
+        res.append(r)
+    return res
+
+
+def propagate_table(system, grid: Grid, rho0, out_ops: Sequence, traj: Trajectories,
+                    pt: Optional[ProcessTensor] = None, ctx=None):
+    """propagate() returning ACE's output table per trajectory: (1 + n_out, window_len) arrays, row 0 = the step
+    times grid.ta + dt * step, row 1 + k = output k (general_system.py:343), assembled on the device
+    (pqd_propagate_table) so the arrays are views of one host buffer."""
+    ctx = ctx or _lib.context()
+    dim = _systems(system)[0].dim
+    off, _ = table_offsets(traj, len(out_ops))
+    n_tab = int(off[-1])
+    with ctx.lock:
+        keep, total = _prep(system, grid, rho0, out_ops, traj, pt, ctx)
+        k1, k2, r0, ops, sched, sc, gc, tc, tsys, n_sys = keep
+        table = np.empty(max(1, n_tab), dtype=np.complex128)
+        pth = pt.handle(ctx, dim) if pt is not None else None
+        _lib.check(_lib.lib().pqd_propagate_table(ctx.handle, n_sys, sc, _lib.iptr(tsys), C.byref(gc), pth,
+                                                  _lib.iptr(sched), _lib.cptr(r0), len(out_ops), _lib.cptr(ops),
+                                                  C.byref(tc), _lib.cptr(table), max(1, n_tab)))
+    return split_table(table, traj, len(out_ops))
+
+
 def free_propagators(system: System, grid: Grid, ctx=None):
     """M[2n + h] = free propagator of half step h of step n (N^2 x N^2, row-major vec convention)"""
     ctx = ctx or _lib.context()
@@ -319,6 +365,14 @@ class Plan:
         t = torch.empty(max(1, self.total), dtype=torch.complex128, device=dev)
         _lib.check(_lib.lib().pqd_plan_copy_output(self.handle, C.c_void_p(t.data_ptr()), max(1, self.total)))
         return t[: self.total]
+
+    def download_table(self):
+        """the outputs as ACE tables (propagate_table's layout): list of (1 + n_out, window_len) views"""
+        n = C.c_int64()
+        _lib.check(_lib.lib().pqd_plan_table_len(self.handle, C.byref(n)))
+        table = np.empty(max(1, n.value), dtype=np.complex128)
+        _lib.check(_lib.lib().pqd_plan_download_table(self.handle, _lib.cptr(table), max(1, n.value)))
+        return split_table(table, self.traj, self.n_out)
 
     def download(self):
         out = np.zeros(max(1, self.total), dtype=np.complex128)

@@ -28,7 +28,7 @@ import numpy as np
 from ..constants import hbar
 from .. import constants
 from .. import opgrammar
-from ..engine import Grid, MTO, ProcessTensor, System, Trajectories, free_propagators, propagate, KIND
+from ..engine import Grid, MTO, ProcessTensor, System, Trajectories, free_propagators, propagate, propagate_table, KIND
 
 temp_dir = constants.temp_dir
 
@@ -326,6 +326,11 @@ def system_ace_stream(t_start, t_end, *pulses, dt=0.01, phonons=False, t_mem=20.
     multi = len(systems) > 1
     tr = Trajectories(np.array(begins), np.array(ends), mtos, system=np.array(traj_sys) if multi else None)
     from .. import _lib
+    if n_real:
+        # ACE's output table per trajectory, assembled on the device (pqd_propagate_table): views, no host copies
+        res = propagate_table(systems if multi else system, grid, rho_init, out_mats, tr, pt=pt,
+                              ctx=_lib.context(device))
+        return res if trajectories is not None else res[0]
     outs = propagate(systems if multi else system, grid, rho_init, out_mats, tr, pt=pt, ctx=_lib.context(device))
     results = []
     for k, o in enumerate(outs):

@@ -19,6 +19,7 @@ Scalars are complex Python numbers, operators are numpy (d, d) complex arrays; `
 operators is the matrix product, `otimes` the Kronecker product (left factor = most significant).
 """
 import cmath
+import functools
 import re
 
 import numpy as np
@@ -198,7 +199,13 @@ def evaluate(text):
 
 
 def to_matrix(text, dim=None):
-    """Operator string -> (dim, dim) complex matrix; a bare scalar is promoted to scalar*Id."""
+    """Operator string -> (dim, dim) complex matrix; a bare scalar is promoted to scalar*Id. Parses are cached per
+    (text, dim) (a two-time sweep lowers the same MTO strings once per trajectory); every call returns a fresh array."""
+    return _to_matrix_cached(str(text), dim).copy()
+
+
+@functools.lru_cache(maxsize=4096)
+def _to_matrix_cached(text, dim):
     v = evaluate(text)
     if not _is_op(v):
         if dim is None:

@@ -72,12 +72,15 @@ def sixls_linear(t_start, t_end, *pulses, dt=0.5, delta_b=4, gamma_e=1/100, gamm
     if fwd.get("trajectories") is not None:
         # per-trajectory magnetic fields (an e0 x bx scan in one launch): a spec's "bx" / "bz" become its own
         # system_op, the strings this function writes for those fields
-        specs = []
+        specs, field_ops = [], {}
         for spec in fwd["trajectories"]:
             if "bx" in spec or "bz" in spec:
                 spec = dict(spec)
-                spec["system_op"] = sixls_ops(delta_b, gamma_e, gamma_b, gamma_d, spec.pop("bx", bx),
-                                              spec.pop("bz", bz), lindblad, rf, d0, d1, d2)[0]
+                key = (spec.pop("bx", bx), spec.pop("bz", bz))
+                if key not in field_ops:
+                    field_ops[key] = sixls_ops(delta_b, gamma_e, gamma_b, gamma_d, key[0], key[1], lindblad, rf,
+                                               d0, d1, d2)[0]
+                spec["system_op"] = field_ops[key]
             specs.append(spec)
         fwd["trajectories"] = specs
     result = system_ace_stream(

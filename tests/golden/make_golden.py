@@ -345,6 +345,9 @@ def gen_twotime_anchor():
     L.context = lambda device=None: None  # noqa: E731  (no device in the build container)
     gs.propagate = lambda system, grid, rho0, out_ops, traj, pt=None, ctx=None: oracle.propagate(  # noqa: E731
         system, grid, rho0, out_ops, traj, pt=pt, nthreads=8)
+    from pyaceqd_amd.engine import tables_from_outputs
+    gs.propagate_table = lambda system, grid, rho0, out_ops, traj, pt=None, ctx=None: tables_from_outputs(  # noqa
+        gs.propagate(system, grid, rho0, out_ops, traj, pt=pt), traj, grid)
     p = ChirpedPulse(tau_0=1.0, e_start=-2.0, e0=1.3, t0=1.5, polar_x=0.8)
     t_axis = np.round(np.arange(8) * 0.5, 6)
     rho0 = np.zeros((4, 4), dtype=complex)

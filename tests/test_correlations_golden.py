@@ -64,9 +64,13 @@ def _oracle_propagation(monkeypatch):
     from oracle import oracle
     import pyaceqd_amd._lib as L
     from pyaceqd_amd.general_system import general_system as gs
+    from pyaceqd_amd.engine import tables_from_outputs
     monkeypatch.setattr(L, "context", lambda device=None: None)
     monkeypatch.setattr(gs, "propagate", lambda system, grid, rho0, out_ops, traj, pt=None, ctx=None: oracle.propagate(
         system, grid, rho0, out_ops, traj, pt=pt, nthreads=4))
+    monkeypatch.setattr(gs, "propagate_table", lambda system, grid, rho0, out_ops, traj, pt=None, ctx=None:
+                        tables_from_outputs(oracle.propagate(system, grid, rho0, out_ops, traj, pt=pt, nthreads=4),
+                                            traj, grid))
 
 
 # ------------------------------------------------------------------------------------------- trajectory drivers

@@ -140,6 +140,30 @@ def test_sweep_pt_many_trajectories_and_ragged_windows():
               oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
 
 
+@pytest.mark.parametrize("chi", [1, 32, 64])
+def test_output_tables_match_flat_outputs(chi):
+    """pqd_propagate_table / Plan.download_table (ACE's table per trajectory, assembled on the device) hold exactly
+    the flat outputs plus the time row (ragged windows, two systems, the no-PT, quad and batched paths)"""
+    N = 2 if chi == 32 else 4
+    s1, grid = H.random_system(N, n_steps=40, seed=3, ta=-1.25)
+    s2, _ = H.random_system(N, n_steps=40, seed=4, ta=-1.25)
+    pt = ptmod.random_pt(N, chi, D=N * N, n_slices=41, seed=5, eps=0.1) if chi > 1 else None
+    tr = _traj(grid.n_steps, N, 21, seed=2)
+    tr = Trajectories(tr.out_begin, tr.out_end, tr.mtos, system=np.arange(tr.n_traj) % 2)
+    ops = [H.ketbra(N, a, b) for a in range(N) for b in range(N)][:5]
+    rho0 = H.random_rho(N)
+    flat = engine.propagate([s1, s2], grid, rho0, ops, tr, pt=pt)
+    want = engine.tables_from_outputs(flat, tr, grid)
+    got = engine.propagate_table([s1, s2], grid, rho0, ops, tr, pt=pt)
+    assert len(got) == len(want)
+    for g, w in zip(got, want):
+        assert g.shape == w.shape and np.array_equal(g, w)
+    plan = engine.Plan([s1, s2], grid, rho0, ops, tr, pt=pt)
+    plan.execute()
+    for g, w in zip(plan.download_table(), want):
+        assert np.array_equal(g, w)
+
+
 def test_empty_batch_and_zero_steps():
     sysd, grid = H.random_system(2, n_steps=0, seed=0)
     tr = Trajectories(np.array([0]), np.array([0]))
@@ -326,6 +350,8 @@ def _oracle_patch(monkeypatch):
     def prop(system, grid, rho0, out_ops, traj, pt=None, ctx=None):
         return oracle.propagate(system, grid, rho0, out_ops, traj, pt=pt, nthreads=8)
     monkeypatch.setattr(gs, "propagate", prop)
+    monkeypatch.setattr(gs, "propagate_table", lambda system, grid, rho0, out_ops, traj, pt=None, ctx=None:
+                        engine.tables_from_outputs(prop(system, grid, rho0, out_ops, traj, pt), traj, grid))
 
 
 def test_tls_rabi_kat():

@@ -20,6 +20,8 @@ import os
 import re
 
 import numpy as np
+
+from pyaceqd_amd.engine import tables_from_outputs
 import pytest
 
 from pyaceqd_amd import opgrammar
@@ -42,6 +44,8 @@ def _capture(monkeypatch):
         return [np.zeros((int(e - b + 1), len(out_ops)), dtype=complex) for b, e in zip(traj.out_begin, traj.out_end)]
     monkeypatch.setattr(L, "context", lambda device=None: None)
     monkeypatch.setattr(gs, "propagate", prop)
+    monkeypatch.setattr(gs, "propagate_table", lambda system, grid, rho0, out_ops, traj, pt=None, ctx=None:
+                        tables_from_outputs(prop(system, grid, rho0, out_ops, traj, pt, ctx), traj, grid))
     return got
 
 
