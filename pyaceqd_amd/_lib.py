@@ -117,6 +117,8 @@ def lib():
                     raise PQDError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
                 L = C.CDLL(LIB_PATH)
                 for name, (args, res) in _SIGS.items():
+                    if os.environ.get("PQD_LIB") and not hasattr(L, name):
+                        continue  # A/B against an older build: entry points it predates stay unbound
                     f = getattr(L, name)
                     f.argtypes = args
                     f.restype = res

@@ -551,6 +551,15 @@ static hipError_t launch_free_prop_pass(int N2, const FreePropParams& p, hipStre
     }
 }
 
+// the pulse windows alone (plan creation decides from them whether windows pay, pqd_host.cpp)
+hipError_t launch_free_win(const FreePropParams& p, hipStream_t s) {
+    if (!p.win || p.n_steps <= 0 || p.n_sys <= 0) return hipSuccess;
+    hipLaunchKernelGGL(free_win_init_kernel, dim3((p.n_sys + 255) / 256), dim3(256), 0, s, p.win, p.n_sys);
+    const long long nblk = (long long)p.n_sys * ((2LL * p.n_steps + 255) / 256);
+    hipLaunchKernelGGL(free_win_kernel, dim3((unsigned)std::min<long long>(nblk, FP_MAX_BLOCKS)), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
 // with p.Midle: the idle propagators first (one per system), then (with p.win) the pulse windows, then every half step
 // inside its window (idle ones copy Midle)
 hipError_t launch_free_prop(int N2, const FreePropParams& p, hipStream_t s) {

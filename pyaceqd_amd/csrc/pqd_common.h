@@ -179,6 +179,7 @@ struct FuseParams {          // F(m) = M_a(m) M_b(m-1) (1 <= m < n_steps), W(m) 
 };
 
 hipError_t launch_free_prop(int N2, const FreePropParams& p, hipStream_t s);
+hipError_t launch_free_win(const FreePropParams& p, hipStream_t s);
 // flags |= 1 if any of the n complex values is NaN or Inf (one pass over the output buffer at synchronize: the sweep
 // kernels carry no per-store check, which cost 1.7% of the headline kernel)
 hipError_t launch_check_finite(const double2* v, int64_t n, unsigned* flags, hipStream_t s);

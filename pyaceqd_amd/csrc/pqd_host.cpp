@@ -201,6 +201,7 @@ struct pqd_plan {
     DevBuf<double2> L0, S, T, samples, M, Midle, F, W, rho0, ovec, sop, out;
     DevBuf<double2> Fidle, Widle;  // idle fused operators per system (pulse windows)
     DevBuf<int2> win;              // per-system pulse windows (free_prop.hip free_win_kernel), PQD_WIN=0: none
+    int win_mode = 0;              // PQD_WIN: 1 auto (windows when they leave out >= 10% of the half steps), 2 always
     DevBuf<FreePropSys> systab;
     FuseParams fu{};
     DevBuf<int> sched, blk_traj, blk_end, blk_sys, blk_act, blk_src, traj_sys, wbeg, wend, ev_start;
@@ -884,13 +885,30 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
         HIPCHK(P->Midle.alloc((size_t)n_sys * m2));
         P->fp.Midle = P->Midle.p;
         // pulse windows: half steps outside a system's [first, last] non-idle half step are neither stored nor
-        // re-read (sweeps take Midle / Fidle / Widle there); PQD_WIN=0 stores every half step (A/B)
-        if (const char* we = getenv("PQD_WIN"); !(we && atoi(we) == 0)) {
+        // re-read (kernels take Midle / Fidle / Widle there). PQD_WIN=0 stores every half step, 2 always uses the
+        // windows, 1 (default) uses them when they leave out at least a tenth of the half steps
+        // Windows only where every kernel of the plan reads through them: the quad and no-PT kernels without a
+        // trunk pre-pass (the batched sweep reads every half step as stored; the split path may fall back to it).
+        const bool win_ok = (P->nopt || P->quad) && P->n_trunk == 0;
+        if (const char* we = getenv("PQD_WIN"); win_ok && !(we && atoi(we) == 0)) {
             HIPCHK(P->win.alloc((size_t)n_sys));
             P->fp.win = P->win.p;
+            P->win_mode = we ? atoi(we) : 1;
         }
     }
     P->fp.ta = grid->ta; P->fp.dt = grid->dt; P->fp.n_steps = ns; P->fp.n_sub = grid->n_sub; P->fp.M = P->M.p;
+    if (P->win.p && P->win_mode == 1 && ns > 0) {
+        HIPCHK(launch_free_win(P->fp, s));
+        std::vector<int2> wh(n_sys);
+        HIPCHK(hipMemcpyAsync(wh.data(), P->win.p, sizeof(int2) * n_sys, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        int64_t stored = 0;
+        for (const int2& w : wh) stored += w.y >= w.x ? (int64_t)(w.y - w.x + 1) : 0;
+        if (10 * stored > 9 * (int64_t)n_sys * 2 * ns) {  // windows leave out < 10%: store every half step
+            P->win.release();
+            P->fp.win = nullptr;
+        }
+    }
 
     SweepParams& sp = P->sp;
     sp.M = P->M.p;

@@ -359,9 +359,13 @@ __device__ __forceinline__ void pt_row_mfma16(const double2* __restrict__ Qg, do
 
 // TRUNK: the trunk pre-pass instance (writes checkpoints through p.ck_map); kept out of the main sweep's instance,
 // where the extra live values cost VGPR spills
+// Reads every half step's M, F, W as stored: plans running this kernel (main sweep or trunk pre-pass) build the free
+// propagators without pulse windows (pqd_host.cpp). A window-select form of these loads measured 1.8% slower on the
+// bench launch even with its selects folded away at compile time (202.3 vs 198.1 ms, profiles/r02/windows/).
 template <int N2, int CHI, int BT, bool TRUNK>
-__global__ __launch_bounds__(64 * BT * sweep_wpt(N2, BT, CHI)) void pt_sweep_kernel(SweepParams p, const double2* __restrict__ Qg0,
-                                                                                    double2* __restrict__ outg) {
+__global__ __launch_bounds__(64 * BT * sweep_wpt(N2, BT, CHI)) void pt_sweep_kernel(SweepParams p, const double2* __restrict__ Mg,
+                                                           const double2* __restrict__ Qg0, double2* __restrict__ outg,
+                                                           const double2* __restrict__ Fg, const double2* __restrict__ Wg) {
     using L = SweepLayout<N2, CHI, BT>;
     constexpr int RS = L::RS, TS = L::TS, KD = L::KD, NCOL = L::NCOL;
     constexpr int WPT = L::WPT, NW = L::NW, NT = 64 * NW;  // waves per trajectory, waves, threads
@@ -370,7 +374,6 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(N2, BT, CHI)) void pt_sweep_ker
     double2* rbuf = smem + BT * TS;
     __shared__ int s_traj[BT], s_wb[BT], s_we[BT], s_fz[BT], s_sys[BT], s_act[BT], s_src[BT];
     __shared__ long long s_wo[BT];
-    __shared__ int2 s_win[BT];  // pulse window of the slot's system (fw_M / fw_F / fw_W)
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -385,7 +388,6 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(N2, BT, CHI)) void pt_sweep_ker
         s_wo[tid] = t >= 0 ? p.woff[t] : 0;
         s_fz[tid] = 0;
         s_sys[tid] = t >= 0 ? p.traj_sys[t] : 0;
-        s_win[tid] = fw_win(p, s_sys[tid]);
         s_act[tid] = p.blk_act[blockIdx.x * BT + tid];
         s_src[tid] = p.blk_src[blockIdx.x * BT + tid];
     }
@@ -409,9 +411,11 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(N2, BT, CHI)) void pt_sweep_ker
     const int n_end = p.blk_end[blockIdx.x];
     // a workgroup may mix systems (per-trajectory drives, e.g. one system per scan point): each wave reads the
     // free propagators of its own trajectory's system
-    const int sw = __builtin_amdgcn_readfirstlane(s_sys[tw]);
-    const int2 wwin = make_int2(__builtin_amdgcn_readfirstlane(s_win[tw].x), __builtin_amdgcn_readfirstlane(s_win[tw].y));
-    constexpr int M2 = N2 * N2;
+    {
+        const int sw = __builtin_amdgcn_readfirstlane(s_sys[tw]);
+        Mg += (size_t)sw * p.m_stride;
+        Fg += (size_t)sw * p.f_stride;
+    }
 
     // ---- initial augmented states rho0 (x) bond0 (thread -> column)
     for (int c = tid; c < NCOL; c += NT) {
@@ -450,7 +454,7 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(N2, BT, CHI)) void pt_sweep_ker
     double2 wpre = c_zero();
     if (n0 > 0 && lanetr && tid < ntr) {  // the step the loop starts at: W(n0) row element, as fetched a step ahead
         const int a = tid % N2, bk = tid / N2, b = bk / p.n_out, k = bk - (bk / p.n_out) * p.n_out;
-        wpre = fw_W(p, s_sys[b], s_win[b], n0, N2)[k * N2 + a];
+        wpre = Wg[(size_t)s_sys[b] * p.w_stride + ((size_t)n0 * p.n_out + k) * N2 + a];
     }
     bool fz = false;  // this wave's trajectory sits between M_b(n-1) and M_a(n) unapplied (fused step n)
     for (int n = n0;; ++n) {
@@ -534,7 +538,8 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(N2, BT, CHI)) void pt_sweep_ker
                 if (s_wb[b] <= n && n <= s_we[b]) {
                     double2 s = c_zero();
                     // fused trajectories still hold the state before M_b(n-1): read it through W(n)
-                    const double2* ov = (s_fz[b] ? fw_W(p, s_sys[b], s_win[b], n, N2) : p.ovec) + (size_t)k * N2;
+                    const double2* ov = (s_fz[b] ? Wg + (size_t)s_sys[b] * p.w_stride + (size_t)n * p.n_out * N2
+                                                 : p.ovec) + (size_t)k * N2;
                     // all of a chunk's row loads are issued before its first FMA (one memory round trip per
                     // chunk, not one per few elements: the scheduler otherwise interleaves them)
                     constexpr int CK = N2 <= 16 ? N2 : 9;
@@ -555,18 +560,18 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(N2, BT, CHI)) void pt_sweep_ker
         if (n >= n_end) break;
         if (lanetr && tid < ntr) {  // W(n + 1) row element for the next step's traces (fused trajectories)
             const int a = tid % N2, bk = tid / N2, b = bk / p.n_out, k = bk - (bk / p.n_out) * p.n_out;
-            wpre = fw_W(p, s_sys[b], s_win[b], n + 1, N2)[k * N2 + a];
+            wpre = Wg[(size_t)s_sys[b] * p.w_stride + ((size_t)(n + 1) * p.n_out + k) * N2 + a];
         }
 
         // ------------------------------------------------------------ column phase A
-        const double2* Ma = fw_M(p, sw, wwin, 2 * n, M2);
+        const double2* Ma = Mg + (size_t)(2 * n) * N2 * N2;
         if (!(p.ablate & 2) && n >= my_act) {
             const bool mto_now = ev_cur < ev_lim && p.ev[ev_cur].x == n;
             if (fz && !mto_now) {  // no MTO at step n: M_b(n-1) and M_a(n) in one operator
-                col(fw_F(p, sw, wwin, n, M2));
+                col(Fg + (size_t)n * N2 * N2);
             } else {
                 // a slot activated at n holds the trunk's state with M_b(n-1) still deferred, but has an MTO at n
-                if (fz) col(fw_M(p, sw, wwin, 2 * n - 1, M2));
+                if (fz) col(Mg + (size_t)(2 * n - 1) * N2 * N2);
                 while (ev_cur < ev_lim) {  // applyBefore-false MTOs at step n
                     const int4 e = p.ev[ev_cur];
                     if (e.x != n || e.y != 1) break;
@@ -690,7 +695,7 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(N2, BT, CHI)) void pt_sweep_ker
         __syncthreads();
 
         // ------------------------------------------------------------ column phase B
-        const double2* Mb = fw_M(p, sw, wwin, 2 * n + 1, M2);
+        const double2* Mb = Ma + N2 * N2;
         // fuse M_b(n) into the next step's operator unless this trajectory has an MTO at step n+1
         fz = p.fuse && !(ev_cur < ev_lim && p.ev[ev_cur].x == n + 1);
         if (!(p.ablate & 2) && !fz && n >= my_act) {
@@ -731,9 +736,9 @@ __global__ __launch_bounds__(64) void sweep_nopt_kernel(SweepParams p) {
     const int wb = p.wbeg[t], we = p.wend[t];
     const long long wo = p.woff[t];
     int ev_cur = p.ev_start[t];
-    const int ev_lim = p.ev_start[t + 1];
     const int sy = p.traj_sys[t];
-    const int2 wn = fw_win(p, sy);
+    const int2 wn = fw_win(p, sy);  // pulse windows (pqd_host.cpp: only plans whose kernels all read through them)
+    const int ev_lim = p.ev_start[t + 1];
     double2 own = lane < N2 ? p.rho0[lane] : c_zero();
     while (ev_cur < ev_lim) {
         const int4 e = p.ev[ev_cur];
@@ -785,8 +790,8 @@ hipError_t launch_sw(int n_blocks, const SweepParams& p, hipStream_t s) {
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((pt_sweep_kernel<N2, CHI, BT, TRUNK>), dim3(n_blocks), dim3(64 * L::NW), L::LDS, s, p, p.Q,
-                       p.out);
+    hipLaunchKernelGGL((pt_sweep_kernel<N2, CHI, BT, TRUNK>), dim3(n_blocks), dim3(64 * L::NW), L::LDS, s, p, p.M, p.Q,
+                       p.out, p.F, p.W);
     return hipGetLastError();
 }
 
