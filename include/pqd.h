@@ -171,6 +171,9 @@ int pqd_plan_download_table(pqd_plan* plan, pqd_c128* table, int64_t table_len);
  * trajectory-steps one execute propagates (trajectories of one system that share a lock-step workgroup propagate
  * their common MTO-free trunk once: PQD_BRANCH) */
 int pqd_plan_info(const pqd_plan* plan, int32_t* path, int32_t* bt, int32_t* split_fallbacks, int64_t* traj_steps);
+/* 1 when the plan builds its free propagators through pulse windows (half steps outside a system's first..last driven
+ * half step are not built; its kernels read the idle operators there: DESIGN.md §4.2, PQD_WIN), else 0 */
+int pqd_plan_windows(const pqd_plan* plan, int32_t* on);
 /* average kernel durations (ms) of the executions since the last reset (the most recent 64 at most),
  * from HIP events on the launch stream: [0] free-propagator kernel, [1] sweep kernel; n = executions */
 int pqd_plan_timing(pqd_plan* plan, double* ms_free, double* ms_sweep, int32_t* n, int32_t reset);

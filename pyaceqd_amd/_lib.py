@@ -83,6 +83,7 @@ _SIGS = {
     "pqd_plan_copy_output": ([C.c_void_p, C.c_void_p, C.c_int64], C.c_int),
     "pqd_plan_table_len": ([C.c_void_p, P_I64], C.c_int),
     "pqd_plan_download_table": ([C.c_void_p, P_C128, C.c_int64], C.c_int),
+    "pqd_plan_windows": ([C.c_void_p, P_I32], C.c_int),
     "pqd_plan_info": ([C.c_void_p, P_I32, P_I32, P_I32, P_I64], C.c_int),
     "pqd_plan_timing": ([C.c_void_p, P_F64, P_F64, P_I32, C.c_int32], C.c_int),
     "pqd_plan_destroy": ([C.c_void_p], None),

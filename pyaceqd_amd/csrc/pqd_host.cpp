@@ -1103,6 +1103,12 @@ int pqd_plan_copy_output(pqd_plan* P, void* dst, int64_t out_len) {
     return rc;
 }
 
+int pqd_plan_windows(const pqd_plan* P, int32_t* on) {
+    if (!P || !on) return fail(PQD_ERR_ARG, "NULL argument");
+    *on = P->win.p ? 1 : 0;
+    return PQD_OK;
+}
+
 int pqd_plan_info(const pqd_plan* P, int32_t* path, int32_t* bt, int32_t* split_fallbacks, int64_t* traj_steps) {
     if (!P) return fail(PQD_ERR_ARG, "plan is NULL");
     if (traj_steps) *traj_steps = P->traj_steps;

@@ -348,6 +348,12 @@ class Plan:
         _lib.check(_lib.lib().pqd_plan_info(self.handle, C.byref(p), C.byref(b), C.byref(f), C.byref(n)))
         return self.PATHS[p.value], b.value, f.value
 
+    def windows(self):
+        """True when the free propagators are built through pulse windows"""
+        on = C.c_int32()
+        _lib.check(_lib.lib().pqd_plan_windows(self.handle, C.byref(on)))
+        return bool(on.value)
+
     def traj_steps(self):
         """trajectory-steps one execute propagates (shared trunks counted once per workgroup)"""
         p, b, f, n = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int64()

@@ -1,8 +1,10 @@
 """Pulse windows (free_prop.hip free_win_kernel, pqd_common.h fw_M / fw_F / fw_W). GPU only.
 
-A system's half steps outside [first, last] half step with a non-zero pulse sample are not stored; every sweep kernel
-reads the system's idle operators there (Midle, Fidle = Midle Midle, Widle = ovec . Midle, built with the storing
-kernels' own arithmetic). The outputs must be bit-identical to storing every half step (PQD_WIN=0) on every path —
+A system's half steps outside [first, last] half step with a non-zero pulse sample are not stored; the quad and no-PT
+kernels read the system's idle operators there (Midle, Fidle = Midle Midle, Widle = ovec . Midle, built with the
+storing kernels' own arithmetic). Plans on the batched sweep (or with a trunk pre-pass, or split groups that may fall
+back to it) build every half step, and a window that leaves out less than a tenth is dropped (test_window_selection).
+The outputs must be bit-identical to storing every half step (PQD_WIN=0) on every path —
 quads, the batched sweep, split groups, the no-PT kernel, shared trunks — with several systems of different windows
 in one plan (pulse early, late, two pulses with an idle gap inside the window, never, always), MTOs inside and
 outside the windows, and fused and unfused half steps; and within 1e-11 of the CPU oracle."""
@@ -122,3 +124,20 @@ def test_windows_long_idle_scan(monkeypatch, N, n_sub):
     ops = [H.ketbra(N, 1, 1)]
     rho0 = H.ketbra(N, 0, 0)
     _both(monkeypatch, systems, grid, rho0, ops, tr, pt)
+
+
+@pytest.mark.parametrize("case,win,expect", [("quad", "1", True), ("nopt", "1", True), ("batched", "1", False),
+                                             ("batched", "2", False), ("quad_full", "1", False),
+                                             ("quad_full", "2", True), ("quad", "0", False)])
+def test_window_selection(monkeypatch, case, win, expect):
+    """windows only where every kernel of the plan reads through them (quad, no-PT), only when they leave out at least
+    a tenth of the half steps unless forced (PQD_WIN=2), never with PQD_WIN=0"""
+    monkeypatch.setenv("PQD_WIN", win)
+    N = 3 if case == "batched" else 2
+    n_steps = 60
+    systems, grid = _windowed_systems(N, n_steps, seed=7)
+    systems = [systems[4]] if case == "quad_full" else [systems[0], systems[1]]  # whole run driven / short pulses
+    pt = None if case == "nopt" else ptmod.random_pt(N, 16, D=min(N * N, 4), n_slices=7, seed=3, eps=0.1)
+    tr = Trajectories(np.zeros(8, dtype=int), np.full(8, n_steps), system=np.arange(8) % len(systems))
+    plan = engine.Plan(systems, grid, H.random_rho(N), [H.ketbra(N, 0, 0)], tr, pt=pt)
+    assert plan.windows() == expect
