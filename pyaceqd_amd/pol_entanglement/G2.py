@@ -358,8 +358,7 @@ def densitymatrix_reuse_scan(instances, model_kwargs=None, return_rho=False):
     for x in insts[1:]:
         if x.dt != first.dt or x.tend != first.tend:
             raise ValueError("the points of a scan must share dt and tend")
-    per = [[] for _ in insts]
-    for v in range(3):
+    def variant(v):
         specs, counts, outs, n_tau = [], [], None, None
         for x, k in zip(insts, kw):
             sp, outs, n_tau = x._g2_specs(*x._reuse_variants()[v])
@@ -372,8 +371,16 @@ def densitymatrix_reuse_scan(instances, model_kwargs=None, return_rho=False):
         opts = dict(first.options)
         opts["output_ops"] = outs
         res = first.system(0, first.tend, trajectories=specs, **opts)
-        o = 0
+        got, o = [], 0
         for i, x in enumerate(insts):
-            per[i].append(x._reuse_integrals(res[o: o + counts[i]], len(x._reuse_variants()[v][1]), n_tau))
+            got.append(x._reuse_integrals(res[o: o + counts[i]], len(x._reuse_variants()[v][1]), n_tau))
             o += counts[i]
+        return got
+
+    # the three launches go through the context lock one at a time; a variant's host work (spec assembly, the
+    # tau/t1 integrals) runs beside the next variant's launch
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=3) as ex:
+        by_variant = list(ex.map(variant, range(3)))
+    per = [[by_variant[v][i] for v in range(3)] for i in range(len(insts))]
     return [x._densitymatrix_from(G, return_rho=return_rho) for x, G in zip(insts, per)]
