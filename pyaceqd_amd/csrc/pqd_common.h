@@ -102,6 +102,7 @@ struct SweepParams {
     int split_b128;          // split groups: 16-B sc1 exchange accesses (A/B switch, PQD_SPLIT_B128 at plan creation)
     unsigned* flags;         // bit 0: a non-finite output value (set by launch_check_finite at synchronize)
     unsigned spin_limit;     // split groups: polls before a wait for the peers times out (PQD_SPLIT_SPIN, tests)
+    int traj_base;           // split groups: trajectory of group 0 (a batch run as several co-resident launches)
     int n_steps;             // grid steps (operand prefetch bound)
     int n_blk;               // blocks of the launch (quad kernel: quads; tail workgroups check it)
     const int2* win;         // per-system pulse windows (FreePropParams::win) or NULL; outside them M, F, W are the
@@ -212,7 +213,7 @@ int tl_dynmap_nmax();
 bool split_supported(int N2, int CHI, int n_traj, int n_cu);
 int split_blocks_per_cu(int N2, int CHI);
 hipError_t launch_split(int N2, int CHI, int n_traj, const SweepParams& p, double2* X, unsigned* cnt,
-                        unsigned* err, hipStream_t s);
+                        unsigned* err, hipStream_t s, int chunk = 0);
 bool sweep_supported(int N2, int CHI);
 // the register-resident TLS sweep (pt_quad.hip): four trajectories per block, CHI/16 waves each
 bool quad_supported(int N2, int CHI);

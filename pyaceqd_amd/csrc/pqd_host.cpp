@@ -210,6 +210,7 @@ struct pqd_plan {
     // trunk pre-pass (pqd_host.cpp plan_trunks): one MTO-free trajectory per system writes the checkpoints the
     // main sweep's slots start from
     int n_trunk = 0, tk_blocks = 0, tk_BT = 4;
+    int tk_chunk = 0;  // split trunks per launch when they do not all fit the device at once (0: one launch)
     bool tk_split = false;
     SweepParams tk{};
     DevBuf<double2> ck, tk_out, tk_Xs;
@@ -526,7 +527,13 @@ static int plan_trunks(pqd_plan* P, pqd_ctx* ctx, int n_sys, const std::vector<s
     const int bpc = split_blocks_per_cu(N2, CHI);
     const char* e = getenv("PQD_SPLIT");
     const int mode = e ? atoi(e) : 1;
-    P->tk_split = mode != 0 && N2 >= 9 && bpc >= 1 && split_supported(N2, CHI, nt, n_cu * bpc);
+    // more trunks than the device holds as co-resident groups: consecutive launches of as many as fit (C5 tomography:
+    // 8 six-level trunks = 288 workgroups on 256 CUs -> 7 + 1; a group steps ~7x faster than a batched block)
+    const int fit = bpc >= 1 ? (n_cu * bpc) / N2 : 0;
+    P->tk_chunk = fit >= 1 && nt > fit ? fit : 0;
+    P->tk_split = mode != 0 && N2 >= 9 && bpc >= 1 && fit >= 1 &&
+                  split_supported(N2, CHI, std::min(nt, fit), n_cu * bpc) &&
+                  nt <= (N2 >= 25 ? 4 : 2) * fit;  // launches in a row still beat one batched pass (§4.6 latencies)
     HIPCHK(P->tk_Xs.alloc((size_t)nt * 2 * N2 * CHI));
     HIPCHK(P->tk_cnt.alloc((size_t)nt * 32));
     HIPCHK(P->tk_err.alloc(4));
@@ -559,7 +566,8 @@ static hipError_t launch_main(pqd_plan* P, hipStream_t s) {
 
 static hipError_t launch_trunks(pqd_plan* P, hipStream_t s) {
     if (!P->n_trunk) return hipSuccess;
-    if (P->tk_split) return launch_split(P->N2, P->CHI, P->n_trunk, P->tk, P->tk_Xs.p, P->tk_cnt.p, P->tk_err.p, s);
+    if (P->tk_split)
+        return launch_split(P->N2, P->CHI, P->n_trunk, P->tk, P->tk_Xs.p, P->tk_cnt.p, P->tk_err.p, s, P->tk_chunk);
     return launch_sweep(P->N2, P->CHI, P->tk_BT, P->tk_blocks, P->tk, s);
 }
 

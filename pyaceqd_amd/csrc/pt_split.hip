@@ -87,7 +87,8 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
     __shared__ int s_abort;
 
     const int tid = threadIdx.x;
-    const int t = blockIdx.x / G, g = blockIdx.x - t * G;
+    const int tl = blockIdx.x / G, g = blockIdx.x - tl * G;
+    const int t = p.traj_base + tl;
     const int wb = p.wbeg[t], we = p.wend[t];
     const long long wo = p.woff[t];
     const int sy = p.traj_sys[t];
@@ -332,19 +333,28 @@ bool split_supported(int N2, int CHI, int n_traj, int n_cu) {
            (long long)n_traj * N2 <= n_cu;
 }
 
-// X: n_traj * 2 * N2 * CHI exchange buffer; cnt: n_traj * 32 counters and err, zeroed here before every launch
+// X: n_traj * 2 * N2 * CHI exchange buffer; cnt: n_traj * 32 counters and err, zeroed here before every launch.
+// chunk > 0: at most `chunk` trajectories per launch (each launch's groups co-resident), launched one after the other
 hipError_t launch_split(int N2, int CHI, int n_traj, const SweepParams& p, double2* X, unsigned* cnt,
-                        unsigned* err, hipStream_t s) {
+                        unsigned* err, hipStream_t s, int chunk) {
     hipError_t e = hipMemsetAsync(cnt, 0, (size_t)n_traj * 32 * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(err, 0, 4 * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
-    switch (N2) {
-        case 4: return launch_split_n<4>(CHI, n_traj, p, X, cnt, err, s);
-        case 9: return launch_split_n<9>(CHI, n_traj, p, X, cnt, err, s);
-        case 16: return launch_split_n<16>(CHI, n_traj, p, X, cnt, err, s);
-        case 25: return launch_split_n<25>(CHI, n_traj, p, X, cnt, err, s);
-        case 36: return launch_split_n<36>(CHI, n_traj, p, X, cnt, err, s);
-        default: return hipErrorInvalidValue;
+    if (chunk <= 0 || chunk > n_traj) chunk = n_traj;
+    for (int base = 0; base < n_traj; base += chunk) {
+        SweepParams q = p;
+        q.traj_base = base;
+        const int n = n_traj - base < chunk ? n_traj - base : chunk;
+        switch (N2) {
+            case 4: e = launch_split_n<4>(CHI, n, q, X, cnt, err, s); break;
+            case 9: e = launch_split_n<9>(CHI, n, q, X, cnt, err, s); break;
+            case 16: e = launch_split_n<16>(CHI, n, q, X, cnt, err, s); break;
+            case 25: e = launch_split_n<25>(CHI, n, q, X, cnt, err, s); break;
+            case 36: e = launch_split_n<36>(CHI, n, q, X, cnt, err, s); break;
+            default: return hipErrorInvalidValue;
+        }
+        if (e != hipSuccess) return e;
     }
+    return hipSuccess;
 }
