@@ -6,7 +6,7 @@ algorithmic flops (fused half steps: F = 8 (D chi^2 + chi N^4 + n_out N^2), D = 
   c2      TLS, N=2, synthetic chi=32 PT, 10,000 steps, 2048 trajectories (area scan)
   c3one   biexciton, N=4, chi=64, 10,000 steps, ONE trajectory (the reference's single-run case: latency)
   c2one   TLS, N=2, chi=32, 10,000 steps, one trajectory;  c5one: six-level, N=6, chi=64, one trajectory
-  c3eight eight biexciton runs (a small area scan), chi=64, 10,000 steps
+  c3eight eight biexciton runs (a small area scan), chi=64, 10,000 steps; c3twenty: twenty; c5eight: eight six-level runs
   c5      six-level linear model, N=6, chi=64, 32 scan points x 64 t1 points = 2048 trajectories, 2,000 tau steps
   c5d     c5 with a dictionary PT (9 slices for the 36 rows, as a generated physical PT has)
   c3d     the bench workload at n_tau = 2,000 with a dictionary PT (9 slices for the 16 rows)
@@ -109,6 +109,8 @@ CONFIGS = {
     "c2one": dict(model="tls", n_scan=1, n_t1=1, n_tau=10000, chi=32),
     "c5one": dict(model="sixls", n_scan=1, n_t1=1, n_tau=10000, chi=64),
     "c3eight": dict(model="biexciton", n_scan=8, n_t1=1, n_tau=10000, chi=64),
+    "c3twenty": dict(model="biexciton", n_scan=20, n_t1=1, n_tau=10000, chi=64),
+    "c5eight": dict(model="sixls", n_scan=8, n_t1=1, n_tau=10000, chi=64),
     "c5": dict(model="sixls", n_scan=32, n_t1=64, n_tau=2000, chi=64),
     "c5d": dict(model="sixls", n_scan=32, n_t1=64, n_tau=2000, chi=64, dictionary=True),
     "c3d": dict(model="biexciton", n_scan=8, n_t1=256, n_tau=2000, chi=64, dictionary=True),

@@ -97,6 +97,26 @@ def test_sweep_pt_split_groups(monkeypatch, N, chi, split):
               oracle.propagate(systems, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
 
 
+@pytest.mark.parametrize("N", [3, 4, 6])
+def test_sweep_pt_split_groups_in_consecutive_launches(N):
+    """a small batch just above the co-resident capacity (n_traj * N^2 > CUs) runs its split groups as consecutive
+    launches (auto mode): same outputs as the oracle and the batched kernel, and the plan reports split groups"""
+    chi = 16
+    systems = [H.random_system(N, n_steps=30, seed=70 + k)[0] for k in range(2)]
+    grid = Grid(0.0, 0.1, 30)
+    n_traj = 256 // (N * N) + 2
+    tr = _traj(grid.n_steps, N, n_traj, seed=3 * N)
+    tr.system = np.array([k % 2 for k in range(n_traj)])
+    pt = ptmod.random_pt(N, chi, D=min(N * N, 9), n_slices=9, seed=N, eps=0.15)
+    ops = [H.ketbra(N, 0, 0), H.ketbra(N, 1, 0)]
+    rho0 = H.random_rho(N)
+    plan = engine.Plan(systems, grid, rho0, ops, tr, pt=pt)
+    plan.execute()
+    got = plan.download()
+    assert plan.info()[0] == "split groups" and plan.info()[2] == 0
+    cmp_lists(got, oracle.propagate(systems, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
+
+
 def test_sweep_pt_split_full_c3_single_run(monkeypatch):
     """C3 single run (one biexciton trajectory, chi = 64, 2000 steps): split groups vs the batched kernel"""
     N, chi = 4, 64
