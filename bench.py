@@ -81,11 +81,15 @@ def flops_per_traj_step(N=4, chi=64, n_out=2, fused=True):
     return 8 * (D * chi * chi + (1 if fused else 2) * chi * N ** 4 + n_out * N * N)
 
 
-def bytes_per_launch(n_steps, n_init, chi, N=4, n_out=2, n_traj=1, D=16, executed_steps=0):
-    """unique HBM bytes one sweep launch must move: every distinct PT slice once, both free propagators
-    per step, per-trajectory outputs written, augmented states never leave LDS"""
+def bytes_per_launch(n_steps, n_init, chi, N=4, n_out=2, n_sys=1, D=16, executed_steps=0):
+    """unique HBM bytes one sweep launch must move: every distinct PT slice once; per system and step the fused
+    operator F(n) (N^2 x N^2) and the output rows W(n) (n_out x N^2) the sweep reads; the outputs written. The
+    augmented states never leave LDS. At the bench config: 411 x 1 MiB + 8 x 10,255 x (4 KiB + 0.5 KiB) + 2 x 16 B
+    x 20.48 M = 0.43 + 0.38 + 0.66 = 1.47 GB"""
     slices = min(n_steps, n_init) + 1
-    return slices * D * chi * chi * 16 + 2 * n_steps * (N * N) ** 2 * 16 + n_out * 16 * executed_steps
+    N2 = N * N
+    return (slices * D * chi * chi * 16 + n_sys * n_steps * (N2 * N2 + n_out * N2) * 16
+            + n_out * 16 * executed_steps)
 
 
 def pmc_traffic(cfg):
@@ -254,20 +258,23 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, ms_sweep, ms_free = [float(x) for x in t.tolist()]
 
-    # the one collective (outside the timed region): every rank's output block gathered in rank order through a
-    # device-buffer all_gather (RCCL over xGMI; scan.gather_tensor); then a finite check of the whole result
+    # the one collective (outside the timed region): every rank's output block gathered to rank 0 in rank order,
+    # device buffer to device buffer (RCCL over xGMI point-to-point; scan.gather_tensor); then a finite check of the
+    # whole result on rank 0
     t0g = time.perf_counter()
     on_host = dist is not None and dist.get_backend() == "gloo"  # gloo gathers host tensors
     local_out = plan.output_tensor(device="cpu" if on_host else None)
-    allout = scanmod.gather_tensor(local_out, dist)
+    allout = scanmod.gather_tensor(local_out, dist, dst=0)
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     gather_ms = (time.perf_counter() - t0g) * 1e3
-    assert bool(torch.isfinite(torch.view_as_real(allout)).all()), "non-finite output"
-    gather = {"collective": "all_gather_into_tensor" if dist is not None else "none (one rank)",
-              "backend": (dist.get_backend() if dist is not None else None), "values": int(allout.numel()),
-              "bytes": int(allout.numel()) * 16, "ms": gather_ms,
-              "checksum": float(torch.view_as_real(allout).abs().sum())}
+    gather = None
+    if rank == 0:
+        assert bool(torch.isfinite(torch.view_as_real(allout)).all()), "non-finite output"
+        gather = {"collective": "gather to rank 0 (send/irecv)" if dist is not None else "none (one rank)",
+                  "backend": (dist.get_backend() if dist is not None else None), "values": int(allout.numel()),
+                  "bytes": int(allout.numel()) * 16, "ms": gather_ms,
+                  "checksum": float(torch.view_as_real(allout).abs().sum())}
 
     useful = n_traj * args.n_tau
     executed = plan.traj_steps()   # shared trunks (PQD_BRANCH) counted once per workgroup
@@ -278,6 +285,7 @@ def main():
     wl = {"n_tau": args.n_tau, "traj_per_gpu": n_traj, "chi": args.chi, "scan_points_per_gpu": args.scan,
           "t1_points": args.t1}
     traffic, traffic_src = pmc_traffic(wl)
+    algo_bytes = bytes_per_launch(grid.n_steps, 410, args.chi, n_out=len(ops), n_sys=args.scan, executed_steps=executed)
     mf = pmc_mfma(wl)
     line = {
         "metric": "propagation steps/sec (whole node), 4-level biexciton PT bond-dim 64",
@@ -307,8 +315,8 @@ def main():
                                     f"executed traj-steps per launch",
                      "flop_convention": "8 real flops per complex multiply-add (SURVEY.md §8d); with the default 3M "
                                         "products (PQD_PT_MODE=4, PQD_CMUL3=1) the matrix cores execute 6",
-                     "hbm_algorithmic_GBs": bytes_per_launch(grid.n_steps, 410, args.chi, n_traj=n_traj,
-                                                             executed_steps=executed) / (ms_sweep * 1e-3) / 1e9},
+                     "hbm_algorithmic_bytes_per_launch": algo_bytes,
+                     "hbm_algorithmic_GBs": algo_bytes / (ms_sweep * 1e-3) / 1e9},
     }
     if mf is not None:
         # what the matrix cores actually execute (3M products: 6 real flops per complex MAC), from the counters,

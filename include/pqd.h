@@ -201,6 +201,13 @@ int pqd_four_time_8op(pqd_ctx* ctx, const pqd_c128* dm_1, const pqd_c128* dm_2, 
                       const double* t1, const pqd_c128* precalc, int32_t n_t, double dt, int32_t n_map,
                       int32_t dim, const pqd_c128* ops8, int32_t early_only, int32_t late_t1_only, double tb,
                       int32_t n_precalc, pqd_c128* result);
+/* pqd_four_time_8op restricted to the rows i in [row_lo, row_hi) of the (t1, t2 >= t1) triangle: result(i, i + j)
+ * for those rows, every other element 0. One rank's share of the pair grid split over GPUs (a
+ * load-balanced triangular row split of timebin_tl.f90:255-302's loop over i; python: scan.triangular_rows). */
+int pqd_four_time_8op_rows(pqd_ctx* ctx, const pqd_c128* dm_1, const pqd_c128* dm_2, const pqd_c128* rho_init,
+                           const double* t1, const pqd_c128* precalc, int32_t n_t, double dt, int32_t n_map,
+                           int32_t dim, const pqd_c128* ops8, int32_t early_only, int32_t late_t1_only, double tb,
+                           int32_t n_precalc, int32_t row_lo, int32_t row_hi, pqd_c128* result);
 int pqd_four_time(pqd_ctx* ctx, const pqd_c128* dm_1, const pqd_c128* dm_2, const pqd_c128* rho_init,
                   const double* t1, const pqd_c128* precalc, int32_t n_t, double dt, int32_t n_map, int32_t dim,
                   const pqd_c128* ops4, double tb, int32_t n_precalc, pqd_c128* result);

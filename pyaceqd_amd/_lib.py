@@ -98,6 +98,9 @@ _SIGS = {
                                        P_C128, P_F64, P_F64, P_C128], C.c_int),
     "pqd_four_time_8op": ([C.c_void_p, P_C128, P_C128, P_C128, P_F64, P_C128, C.c_int32, C.c_double, C.c_int32,
                            C.c_int32, P_C128, C.c_int32, C.c_int32, C.c_double, C.c_int32, P_C128], C.c_int),
+    "pqd_four_time_8op_rows": ([C.c_void_p, P_C128, P_C128, P_C128, P_F64, P_C128, C.c_int32, C.c_double,
+                                C.c_int32, C.c_int32, P_C128, C.c_int32, C.c_int32, C.c_double, C.c_int32, C.c_int32,
+                                C.c_int32, P_C128], C.c_int),
     "pqd_four_time": ([C.c_void_p, P_C128, P_C128, P_C128, P_F64, P_C128, C.c_int32, C.c_double, C.c_int32,
                        C.c_int32, P_C128, C.c_double, C.c_int32, P_C128], C.c_int),
     "pqd_dynamics_t1": ([C.c_void_p, P_C128, P_C128, P_C128, P_F64, P_C128, C.c_int32, C.c_double, C.c_int32,

@@ -197,8 +197,10 @@ __global__ __launch_bounds__(64) void mc_tau_pipe_kernel(MapChainParams p) {
     for (int sl = 0; sl < PFD; ++sl) load_row(sl);
     __syncthreads();
     int cur = 0;
+    // padding lanes (tl == TPW when N2 does not divide 64) read trajectory 0's vector: no LDS access past xs[.][63]
+    const int tlx = tl < TPW ? tl : 0;
     auto step = [&](int sl, int k) {
-        const double2* x = xs[cur] + tl * N2;
+        const double2* x = xs[cur] + tlx * N2;
         double2 y = c_zero();
 #pragma unroll
         for (int c = 0; c < N2; ++c) c_fma(y, am[sl][c], x[c]);

@@ -218,4 +218,5 @@ bool sweep_supported(int N2, int CHI);
 // the register-resident TLS sweep (pt_quad.hip): four trajectories per block, CHI/16 waves each
 bool quad_supported(int N2, int CHI);
 // ncg: 4-column groups per wave, 4 (strips of 16 columns, one wave per SIMD) or 2 (strips of 8, two waves per SIMD)
+int quad_qpw(int CHI, int qpw, int ncg);  // quads per workgroup launch_quad instantiates
 hipError_t launch_quad(int CHI, int n_quads, int qpw, int ncg, const SweepParams& p, hipStream_t s);

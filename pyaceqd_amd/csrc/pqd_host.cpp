@@ -805,6 +805,17 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
         be.push_back(end);
         bs.push_back(sy);
     }
+    // quad kernel: strips of 8 columns (twice the waves, two per SIMD) overlap one wave's round trips with the
+    // other's MFMAs: with no more quads than CUs (C2 single run 17.2 -> 13.1 ms), and at chi = 32 with one quad per
+    // workgroup on a full device too (C2 scan 18.9 -> 18.4 ms); chi = 16 full devices keep the 16-column strips.
+    // P->qpw is then set to the quads per workgroup launch_quad instantiates for (CHI, qcg), so that the trunk
+    // estimate below and PQD_QPW mean what the kernel runs
+    if (P->quad) {
+        const int nbq = (int)be.size();
+        P->qcg = (nbq <= n_cu || (P->CHI == 32 && P->qpw == 1)) ? 2 : 4;
+        if (const char* e = getenv("PQD_QCG")) P->qcg = atoi(e) == 2 ? 2 : 4;
+        P->qpw = quad_qpw(P->CHI, P->qpw, P->qcg);
+    }
     // trunk pre-pass instead of in-workgroup chains: every slot starts at its own branch step from a checkpoint
     // of its system's MTO-free trunk, which one trajectory per system propagates first. Chosen (PQD_TRUNK=-1,
     // auto) when the estimated critical path — trunk latency + the longest block from its first activation — is
@@ -842,7 +853,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
         // blocks resident at once: quads (one workgroup of qpw quads per CU) or BT-workgroups as the LDS allows
         int64_t conc = n_cu;
         if (P->quad) {
-            conc = (int64_t)n_cu * (P->CHI == 32 ? 2 : std::max(1, P->qpw));  // chi = 32: two quads per CU either way
+            conc = (int64_t)n_cu * (P->CHI == 32 ? 2 : P->qpw);  // chi = 32: two quads per CU either way
         } else {
             const int64_t lds = ((int64_t)BT * (N2 * (P->CHI + 1) + 4) + (int64_t)BT * N2) * 16;
             conc = (int64_t)n_cu * std::max<int64_t>(1, std::min<int64_t>(4, (160 * 1024) / std::max<int64_t>(1, lds)));
@@ -974,13 +985,6 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     sp.woff = P->woff.p; sp.ev_start = P->ev_start.p; sp.ev = P->ev.p; sp.sop = P->sop.p; sp.out = P->out.p;
     sp.n_steps = ns;
     sp.n_blk = nb;
-    // quad kernel: strips of 8 columns (twice the waves, two per SIMD) overlap one wave's round trips with the
-    // other's MFMAs: with no more quads than CUs (C2 single run 17.2 -> 13.1 ms), and at chi = 32 with one quad per
-    // workgroup on a full device too (C2 scan 18.9 -> 18.4 ms); chi = 16 full devices keep the 16-column strips
-    if (P->quad) {
-        P->qcg = (nb <= n_cu || (P->CHI == 32 && P->qpw == 1)) ? 2 : 4;
-        if (const char* e = getenv("PQD_QCG")) P->qcg = atoi(e) == 2 ? 2 : 4;
-    }
     finalize_trunks(P);
     if (P->split) {
         HIPCHK(P->Xs.alloc((size_t)P->n_traj * 2 * N2 * P->CHI));
@@ -1305,7 +1309,7 @@ int pqd_propagate_tau(pqd_ctx* ctx, const pqd_c128* dm_tl, int32_t n_maps, const
 
 static int four_time_common(pqd_ctx* ctx, FourTimeParams& p, const pqd_c128* dm_1, const pqd_c128* dm_2,
                             const pqd_c128* rho_init, const double* t1, const pqd_c128* precalc, const pqd_c128* ops,
-                            int n_ops, pqd_c128* result, bool dyn) {
+                            int n_ops, pqd_c128* result, bool dyn, int row_lo = 0, int row_hi = INT_MAX) {
     if (!ctx || !dm_1 || !dm_2 || !rho_init || !t1 || !precalc || !result || (!dyn && !ops))
         return fail(PQD_ERR_ARG, "NULL argument");
     if (p.dim < 2 || p.dim > 6) return fail(PQD_ERR_UNSUPPORTED, "dim %d", p.dim);
@@ -1333,7 +1337,7 @@ static int four_time_common(pqd_ctx* ctx, FourTimeParams& p, const pqd_c128* dm_
     } else {
         std::vector<int2> pairs;
         pairs.reserve((size_t)p.n_t * (p.n_t + 1) / 2);
-        for (int i = 0; i < p.n_t; ++i)
+        for (int i = std::max(0, row_lo); i < std::min(p.n_t, row_hi); ++i)
             for (int j = 0; j <= p.n_t - 1 - i; ++j) pairs.push_back(make_int2(i, j));
         HIPCHK(pr.upload(pairs.data(), pairs.size(), s));
         p.pairs = pr.p; p.n_pairs = (int)pairs.size();
@@ -1356,6 +1360,17 @@ int pqd_four_time_8op(pqd_ctx* ctx, const pqd_c128* dm_1, const pqd_c128* dm_2, 
     p.dim = dim; p.n_t = n_t; p.n_map = n_map; p.n_precalc = n_precalc; p.dt = dt; p.tb = tb;
     p.variant = 0; p.early_only = early_only; p.late_t1_only = late_t1_only;
     return four_time_common(ctx, p, dm_1, dm_2, rho_init, t1, precalc, ops8, 8, result, false);
+}
+
+int pqd_four_time_8op_rows(pqd_ctx* ctx, const pqd_c128* dm_1, const pqd_c128* dm_2, const pqd_c128* rho_init,
+                           const double* t1, const pqd_c128* precalc, int32_t n_t, double dt, int32_t n_map,
+                           int32_t dim, const pqd_c128* ops8, int32_t early_only, int32_t late_t1_only, double tb,
+                           int32_t n_precalc, int32_t row_lo, int32_t row_hi, pqd_c128* result) {
+    if (row_lo < 0 || row_hi < row_lo || row_hi > n_t) return fail(PQD_ERR_ARG, "rows [%d, %d) outside [0, %d)", row_lo, row_hi, n_t);
+    FourTimeParams p{};
+    p.dim = dim; p.n_t = n_t; p.n_map = n_map; p.n_precalc = n_precalc; p.dt = dt; p.tb = tb;
+    p.variant = 0; p.early_only = early_only; p.late_t1_only = late_t1_only;
+    return four_time_common(ctx, p, dm_1, dm_2, rho_init, t1, precalc, ops8, 8, result, false, row_lo, row_hi);
 }
 
 int pqd_four_time(pqd_ctx* ctx, const pqd_c128* dm_1, const pqd_c128* dm_2, const pqd_c128* rho_init,

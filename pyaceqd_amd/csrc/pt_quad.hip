@@ -523,15 +523,20 @@ extern "C" int pqd_debug_quad_stamps(unsigned long long* out) {
 
 bool quad_supported(int N2, int CHI) { return N2 == 4 && (CHI == 16 || CHI == 32); }
 
+// the instantiated quads per workgroup for a requested qpw: 1 or (chi = 16 with 16-column strips: 4 quads of one wave
+// each, a 256-thread workgroup) else 2
+int quad_qpw(int CHI, int qpw, int ncg) { return qpw <= 1 ? 1 : (CHI == 16 && ncg != 2 ? 4 : 2); }
+
 hipError_t launch_quad(int CHI, int n_quads, int qpw, int ncg, const SweepParams& p, hipStream_t s) {
     if (n_quads <= 0) return hipSuccess;
+    const int q = quad_qpw(CHI, qpw, ncg);
     switch (CHI) {
         case 16:
-            if (ncg == 2) return qpw >= 2 ? launch_q<16, 2, 2>(n_quads, p, s) : launch_q<16, 1, 2>(n_quads, p, s);
-            return qpw >= 2 ? launch_q<16, 4, 4>(n_quads, p, s) : launch_q<16, 1, 4>(n_quads, p, s);
+            if (ncg == 2) return q == 2 ? launch_q<16, 2, 2>(n_quads, p, s) : launch_q<16, 1, 2>(n_quads, p, s);
+            return q == 4 ? launch_q<16, 4, 4>(n_quads, p, s) : launch_q<16, 1, 4>(n_quads, p, s);
         case 32:
-            if (ncg == 2) return qpw >= 2 ? launch_q<32, 2, 2>(n_quads, p, s) : launch_q<32, 1, 2>(n_quads, p, s);
-            return qpw >= 2 ? launch_q<32, 2, 4>(n_quads, p, s) : launch_q<32, 1, 4>(n_quads, p, s);
+            if (ncg == 2) return q == 2 ? launch_q<32, 2, 2>(n_quads, p, s) : launch_q<32, 1, 2>(n_quads, p, s);
+            return q == 2 ? launch_q<32, 2, 4>(n_quads, p, s) : launch_q<32, 1, 4>(n_quads, p, s);
         default: return hipErrorInvalidValue;
     }
 }

@@ -341,6 +341,66 @@ class PolarizatzionEntanglement():
         return t1, G2_t
 
 
+_PER_POINT_OPTIONS = {"pulse_file_x", "pulse_file_y", "temp_dir"}
+
+
+def _same(a, b):
+    if a is b:
+        return True
+    try:
+        r = a == b
+        return bool(np.all(r)) if isinstance(r, np.ndarray) else bool(r)
+    except (ValueError, TypeError):
+        try:
+            return np.array_equal(np.asarray(a), np.asarray(b))
+        except (ValueError, TypeError):
+            return False
+
+
+def _options_differ(a, b):
+    """option keys (outside the per-point ones) whose values differ between two instances' options"""
+    keys = (set(a) | set(b)) - _PER_POINT_OPTIONS
+    return {k for k in keys if (k in a) != (k in b) or not _same(a.get(k), b.get(k))}
+
+
+def densitymatrix_reuse_scan_sharded(instances, model_kwargs=None, return_rho=False, dist=None, dst=0):
+    """`densitymatrix_reuse_scan` over a scan grid sharded across ranks (one process per GPU,
+    a contiguous block of grid points per rank, e.g. 32 of 256), gathered to rank `dst` on the device.
+
+    Every rank passes the WHOLE grid (`instances`, `model_kwargs`); rank r runs the points
+    scan.shard_range(n, r, world) in its own three launches, packs each point's (concurrence, rho 4 x 4) into 17
+    complex values of one device tensor, and scan.gather_tensor sends the blocks to `dst` (RCCL point-to-point over
+    xGMI; gloo with host tensors). Returns the full list on `dst` (same order and values as the single-process scan),
+    None on the other ranks. The reference runs the same grid as a host loop of per-point ACE runs
+    (rabi_rotations.py:172-198 around pol_entanglement/G2.py:301-356)."""
+    import torch
+    from ..scan import gather_tensor, shard_range
+    insts = list(instances)
+    kw = list(model_kwargs) if model_kwargs is not None else [{}] * len(insts)
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return densitymatrix_reuse_scan(insts, kw, return_rho=return_rho)
+    rank, world = dist.get_rank(), dist.get_world_size()
+    lo, hi = shard_range(len(insts), rank, world)
+    mine = densitymatrix_reuse_scan(insts[lo:hi], kw[lo:hi], return_rho=True) if hi > lo else []
+    packed = np.zeros((len(mine), 17), dtype=np.complex128)
+    for i, (c, rho) in enumerate(mine):
+        packed[i, 0] = c
+        packed[i, 1:] = np.asarray(rho).reshape(16)
+    on_dev = dist.get_backend() != "gloo" and torch.cuda.is_available()
+    dev = f"cuda:{torch.cuda.current_device()}" if on_dev else "cpu"
+    allp = gather_tensor(torch.from_numpy(packed.reshape(-1)).to(dev), dist, dst=dst)
+    if rank != dst:
+        return None
+    allp = allp.cpu().numpy().reshape(-1, 17)
+    if len(allp) != len(insts):
+        raise RuntimeError(f"gathered {len(allp)} points, expected {len(insts)}")
+    out = []
+    for row in allp:
+        c, rho = float(row[0].real), row[1:].reshape(4, 4)
+        out.append((c, rho) if return_rho else c)
+    return out
+
+
 def densitymatrix_reuse_scan(instances, model_kwargs=None, return_rho=False):
     """`calc_densitymatrix_reuse` for every point of a pulse / field scan in three launches in total.
 
@@ -354,10 +414,21 @@ def densitymatrix_reuse_scan(instances, model_kwargs=None, return_rho=False):
     if not insts:
         return []
     kw = list(model_kwargs) if model_kwargs is not None else [{}] * len(insts)
+    if len(kw) != len(insts):
+        raise ValueError(f"{len(kw)} model_kwargs for {len(insts)} instances")
     first = insts[0]
     for x in insts[1:]:
         if x.dt != first.dt or x.tend != first.tend:
             raise ValueError("the points of a scan must share dt and tend")
+        # every point runs through first.system with first.options: anything else would silently compute a point
+        # with another point's model (per-point pulses come from the instance's own pulses / pulse files, per-point
+        # model keywords through model_kwargs)
+        if x.system is not first.system:
+            raise ValueError("the points of a scan must share their model callable (per-point model keywords go in "
+                             "model_kwargs)")
+        diff = _options_differ(first.options, x.options)
+        if diff:
+            raise ValueError(f"the points of a scan must share their options; they differ in {sorted(diff)}")
     def variant(v):
         specs, counts, outs, n_tau = [], [], None, None
         for x, k in zip(insts, kw):

@@ -42,30 +42,62 @@ def gather_blocks(local, dist=None, dst=0):
     return out
 
 
-def gather_tensor(local, dist=None):
-    """Every rank's 1-D tensor (any length, any device) concatenated in rank order, on every rank.
+def gather_tensor(local, dist=None, dst=0):
+    """Every rank's 1-D tensor (any length, any device) concatenated in rank order on rank `dst` (None elsewhere).
 
-    One all_gather of the block lengths, then one all_gather_into_tensor of the blocks padded to the longest, on the
-    tensors' own device: RCCL over xGMI for GPU tensors (the result blocks never pass through host memory), gloo for
-    CPU tensors. Complex blocks travel as their real view. This is the one collective of a sharded sweep (SURVEY.md
-    §8e); the reference assembles its result lists from per-process CSV files (correlations.py:171-183)."""
+    One all_gather of the block lengths (8 B per rank), then point-to-point: every other rank sends its block to
+    `dst`, which receives each one straight into its slice of the result, on the tensors' own device (RCCL over xGMI
+    for GPU tensors, so the result blocks never pass through host memory; gloo for CPU tensors). No padding and no
+    copy of any block to the other ranks: at 8 ranks of 655 MB only rank 0 receives, 7 x 655 MB, where an all_gather
+    would move 8 x 8 x 655 MB. Complex blocks travel as their real view. This is the one collective of a sharded
+    sweep; the reference assembles its result lists from per-process CSV files
+    (correlations.py:171-183)."""
     import torch
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
         return local
-    world = dist.get_world_size()
+    world, rank = dist.get_world_size(), dist.get_rank()
     cplx = local.is_complex()
     x = (torch.view_as_real(local) if cplx else local).reshape(-1).contiguous()
     n = torch.tensor([x.numel()], dtype=torch.int64, device=x.device)
     ns = torch.empty(world, dtype=torch.int64, device=x.device)
     dist.all_gather_into_tensor(ns, n)
     sizes = [int(v) for v in ns.tolist()]
-    m = max(sizes)
-    buf = torch.zeros(max(1, m), dtype=x.dtype, device=x.device)
-    buf[: x.numel()] = x
-    out = torch.empty(world * max(1, m), dtype=x.dtype, device=x.device)
-    dist.all_gather_into_tensor(out, buf)
-    y = torch.cat([out[r * max(1, m): r * max(1, m) + sizes[r]] for r in range(world)])
-    return torch.view_as_complex(y.reshape(-1, 2)) if cplx else y
+    if rank != dst:
+        if x.numel():
+            dist.send(x, dst)
+        return None
+    out = torch.empty(sum(sizes), dtype=x.dtype, device=x.device)
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    reqs = []
+    for r in range(world):
+        seg = out[int(offs[r]): int(offs[r + 1])]
+        if r == dst:
+            seg.copy_(x)
+        elif sizes[r]:
+            reqs.append(dist.irecv(seg, src=r))
+    for q in reqs:
+        q.wait()
+    return torch.view_as_complex(out.reshape(-1, 2)) if cplx else out
+
+
+def triangular_rows(n_t, rank, world):
+    """rows [lo, hi) of an upper-triangular pair grid (row i holds the n_t - i pairs (i, i + j), timebin_tl.f90:255-302)
+    for `rank`, split so that every rank gets about the same number of pairs (the (i, j) cost is
+    about constant per pair, so row i costs n_t - i): boundary b_r is the first row whose cumulative pair count reaches
+    r / world of the total"""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError(f"bad rank/world {rank}/{world}")
+    n_t = int(n_t)
+    cum = np.concatenate([[0], np.cumsum(np.arange(n_t, 0, -1, dtype=np.int64))])  # pairs in rows [0, i)
+    total = int(cum[-1])
+
+    def bound(r):
+        if r <= 0:
+            return 0
+        if r >= world:
+            return n_t
+        return int(np.searchsorted(cum, r * total / world, side="left"))
+    return bound(rank), bound(rank + 1)
 
 
 def run_sharded(units, work, dist=None):

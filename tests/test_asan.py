@@ -58,6 +58,14 @@ def test_oracle_under_asan():
 
 def test_libpqd_host_code_under_asan():
     lib = os.path.join(REPO, "pyaceqd_amd", "libpqd_asan.so")
+    if os.path.exists("/dev/kfd"):
+        pytest.skip("a GPU is visible: the HIP runtime aborts under a preloaded ASan runtime (module docstring)")
+    # built on demand (incremental; not part of __graft_entry__.build())
+    try:
+        subprocess.run(["make", "-s", "-j", "8", "-C", os.path.join(REPO, "pyaceqd_amd", "csrc"), "asan"], check=True,
+                       capture_output=True, timeout=1200)
+    except (OSError, subprocess.SubprocessError) as e:
+        pytest.skip(f"libpqd_asan.so could not be built here: {e}")
     if not os.path.exists(lib):
         pytest.skip("libpqd_asan.so not built (make -C pyaceqd_amd/csrc asan)")
     if os.path.exists("/dev/kfd"):

@@ -1,7 +1,7 @@
 """Multi-rank paths (world_size 2, 127.0.0.1 rendezvous).
 
 CPU (gloo): a pulse-area scan sharded over ranks through the CPU oracle and gathered to rank 0; the device-buffer
-gather (scan.gather_tensor: all_gather_into_tensor of ragged complex blocks) against a local concatenation.
+gather (scan.gather_tensor: point-to-point to rank 0 of ragged complex blocks) against a local concatenation.
 GPU (gloo, two processes on the one GPU of the box): the bench's two-time sweep with its t1 grid sharded over the
 ranks (bench.py --shard t1), each rank propagating its block through libpqd (the batched kernel),
 gathered with scan.gather_tensor and compared bit for bit with one process propagating the whole grid."""
@@ -83,8 +83,8 @@ def _gather_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     n = 3 + 4 * rank  # ragged blocks
     x = torch.arange(n, dtype=torch.float64) * (1 + 1j) + 100 * rank
-    y = gather_tensor(x.to(torch.complex128), dist)
-    q.put((rank, y.numpy()))
+    y = gather_tensor(x.to(torch.complex128), dist, dst=0)
+    q.put((rank, None if y is None else y.numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -101,8 +101,8 @@ def test_gather_tensor_ragged_complex_world2():
         p.join(timeout=120)
         assert p.exitcode == 0
     ref = np.concatenate([np.arange(3 + 4 * r) * (1 + 1j) + 100 * r for r in range(2)])
-    for r in range(2):
-        assert np.array_equal(got[r], ref)
+    assert np.array_equal(got[0], ref)  # gathered to rank 0 only
+    assert got[1] is None
 
 
 N_T1, N_TAU, CHI = 16, 60, 16
@@ -156,3 +156,122 @@ def test_gloo_world2_t1_sharded_sweep_matches_single_process(monkeypatch):
     ref = np.concatenate([r.ravel() for r in plan.download()])
     assert got.shape == ref.shape
     assert np.array_equal(got, ref)
+
+
+def test_triangular_rows_balance_the_pairs():
+    from pyaceqd_amd.scan import triangular_rows
+    for n_t in (0, 1, 5, 128, 1000):
+        for w in (1, 2, 3, 8):
+            b = [triangular_rows(n_t, r, w) for r in range(w)]
+            assert b[0][0] == 0 and b[-1][1] == n_t
+            assert all(b[i][1] == b[i + 1][0] for i in range(w - 1))
+            pairs = [sum(n_t - i for i in range(lo, hi)) for lo, hi in b]
+            assert sum(pairs) == n_t * (n_t + 1) // 2
+            if n_t >= 8 * w:
+                # every rank within one row (at most n_t pairs) of the even share
+                assert max(abs(p - n_t * (n_t + 1) / 2 / w) for p in pairs) <= n_t
+
+
+def _ft8_inputs(n_t=24, dim=3, seed=5):
+    rng = np.random.default_rng(seed)
+    N2 = dim * dim
+    n_map = 2 * n_t + 6
+    mk = lambda n: np.asfortranarray((np.eye(N2)[None] + 2e-2 * (rng.normal(size=(n, N2, N2))  # noqa: E731
+                                                                + 1j * rng.normal(size=(n, N2, N2)))).transpose(1, 2, 0))
+    dm1, dm2 = mk(n_map), mk(n_map)
+    precalc = np.asfortranarray(np.stack([np.linalg.matrix_power(dm1[:, :, -1], 2 ** b) for b in range(8)], axis=2))
+    rho0 = np.zeros(N2, complex)
+    rho0[0] = 1
+    ops = [np.asfortranarray(rng.normal(size=(dim, dim)) + 1j * rng.normal(size=(dim, dim))) for _ in range(8)]
+    dt = 0.1
+    t1 = dt * np.arange(n_t)
+    return (dm1, dm2, rho0, t1, precalc, dt, dim, *ops, False, False, dt * (n_map - 2))
+
+
+def _ft8_worker(rank, world, port, q):
+    try:
+        import torch  # noqa: F401
+        from pyaceqd_amd.timebin.timebin_tl import four_time_8op_sharded
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        got = four_time_8op_sharded(*_ft8_inputs(), dist=dist)
+        if rank == 0:
+            q.put(("ok", got))
+        else:
+            assert got is None
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put(("err", rank, repr(e)))
+        raise
+
+
+def _spawn2(target):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    msg = q.get(timeout=180)
+    if msg[0] != "ok":
+        for p in procs:
+            p.kill()
+        pytest.fail(f"rank {msg[1]}: {msg[2]}")
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return msg[1]
+
+
+@pytest.mark.gpu
+def test_gloo_world2_four_time_8op_triangular_split_matches_single_process():
+    """the pair triangle of four_time_8op split over two ranks by scan.triangular_rows (two processes on the one GPU),
+    gathered to rank 0: bit-identical to one process computing every row"""
+    from pyaceqd_amd.timebin.timebin_tl import four_time_8op
+    got = _spawn2(_ft8_worker)
+    ref = four_time_8op(*_ft8_inputs())
+    assert np.array_equal(got, ref)
+    assert np.count_nonzero(ref) == 24 * 25 // 2
+
+
+def _c5_worker(rank, world, port, q):
+    try:
+        import tempfile
+        from tests.test_gpu_c5 import BXS, E0S, _point, _pt
+        from pyaceqd_amd.pol_entanglement.G2 import densitymatrix_reuse_scan_sharded
+        from pyaceqd_amd.six_level_system.linear import sixls_linear
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        pt = _pt()
+        with tempfile.TemporaryDirectory() as td:
+            insts = [_point(sixls_linear, e0, pt, td) for e0 in E0S for bx in BXS]
+            got = densitymatrix_reuse_scan_sharded(insts, [{"bx": bx} for e0 in E0S for bx in BXS], return_rho=True,
+                                                   dist=dist)
+        if rank == 0:
+            q.put(("ok", got))
+        else:
+            assert got is None
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put(("err", rank, repr(e)))
+        raise
+
+
+@pytest.mark.gpu
+def test_gloo_world2_c5_scan_sharded_matches_single_process(tmp_path):
+    """BASELINE config 5's tomography scan sharded over two ranks (a contiguous block of grid points
+    per rank, two processes on the one GPU), (concurrence, rho) gathered to rank 0: bit-identical to the scan in one
+    process"""
+    from tests.test_gpu_c5 import BXS, E0S, _point, _pt
+    from pyaceqd_amd.pol_entanglement.G2 import densitymatrix_reuse_scan
+    from pyaceqd_amd.six_level_system.linear import sixls_linear
+    got = _spawn2(_c5_worker)
+    pt = _pt()
+    insts = [_point(sixls_linear, e0, pt, tmp_path) for e0 in E0S for bx in BXS]
+    ref = densitymatrix_reuse_scan(insts, [{"bx": bx} for e0 in E0S for bx in BXS], return_rho=True)
+    assert len(got) == len(ref) == 4
+    for (cg, rg), (cr, rr) in zip(got, ref):
+        assert cg == cr
+        assert np.array_equal(rg, rr)
