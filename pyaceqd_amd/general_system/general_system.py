@@ -89,6 +89,14 @@ def generate_pulsefiles(t, pulses, temp_dir, system_prefix, suffix, abs_only=Fal
     return fx, fy
 
 
+def _ace_file_samples(t, *fs):
+    """What ACE reads back from a pulse / rf file the reference writes (general_system.py:55-71, 84, 213): the
+    grid np.arange(t_start, t_end, dt) and the samples, each printed with %.8f (tools.export_csv precision=8) and
+    parsed again. Returns (t, f...) exactly as read_pulse_file would return them from that text."""
+    q = lambda x: np.asarray(np.char.mod("%.8f", np.asarray(x, dtype=float)), dtype=float)  # noqa: E731
+    return (q(t),) + tuple(q(np.real(f)) + 1j * q(np.imag(f)) for f in fs)
+
+
 def _sample_pulses(pulses, t, abs_only=False):
     px = np.zeros_like(t, dtype=complex)
     py = np.zeros_like(t, dtype=complex)
@@ -163,7 +171,7 @@ def system_ace_stream(t_start, t_end, *pulses, dt=0.01, phonons=False, t_mem=20.
                       prepare_only=False, LO_params=None, dressedstates=False, rf_op=None, rf_file=None,
                       firstonly=False, J_to_file=None, J_file=None, factor_ah=None, use_infinite=False,
                       print_H=False, calc_dynmap=False, rho0=None, get_M_t=None, trajectories=None, n_sub=1,
-                      device=None):
+                      device=None, pulse_sampling="exact"):
     """Propagate one trajectory (or a batch: `trajectories`) and return ACE's output table.
 
     Returns (1 + len(output_ops), n_t) complex, row 0 = time (general_system.py:104-110, 343).
@@ -172,7 +180,16 @@ def system_ace_stream(t_start, t_end, *pulses, dt=0.01, phonons=False, t_mem=20.
     optionally "out_begin", a per-trajectory drive "pulses" / "pulse_file_x" / "pulse_file_y" and per-trajectory
     "system_op" / "lindblad_ops" replacing the call's): a list of per-trajectory results, all propagated in one launch
     (one System per distinct drive and generator: parameter scans over pulses and fields).
+
+    pulse_sampling: "exact" (default) samples the analytic pulses at dt/(4 n_sub), so every exponential midpoint
+    is a sample. "ace_file" gives the pulses the semantics of the files the reference hands ACE
+    (general_system.py:55-71, 213-223): samples on np.arange(t_start, t_end, dt) quantised to %.8f, linearly
+    interpolated between samples and held past t_end - dt, exactly as an explicit pulse_file_x/_y is read (and
+    the rf frequency likewise, :73-84). The two differ by O(dt^2 f'') (about 1e-4 relative for tau_0 = 3 ps at
+    dt = 0.1), which is above the no-phonon 1e-8 tolerance: use "ace_file" to compare against ACE output.
     """
+    if pulse_sampling not in ("exact", "ace_file"):
+        raise ValueError(f"pulse_sampling must be 'exact' or 'ace_file', not {pulse_sampling!r}")
     sanity_checks(system_op, phonons, boson_op, initial, interaction_ops, verbose)
     if multitime_op is not None:
         if isinstance(multitime_op, dict):
@@ -229,6 +246,8 @@ def system_ace_stream(t_start, t_end, *pulses, dt=0.01, phonons=False, t_mem=20.
     # ---------------------------------------------------------------- pulse channels
     ds = dt / (4 * n_sub)
     ts = t_start + ds * np.arange(4 * n_sub * n_steps + 1)
+    # the reference's pulse-file grid (:213); a batch shares one file per drive, up to its longest trajectory
+    t_file = np.arange(t_start, t_start + n_steps * dt if trajectories is not None else t_end, step=dt / 1)
 
     def make_system(pulse_list, pfx, pfy, H0, lind):
         channels, t0s, dts = [], [], []
@@ -249,7 +268,14 @@ def system_ace_stream(t_start, t_end, *pulses, dt=0.01, phonons=False, t_mem=20.
             if pfy is not None:
                 ty, fy = read_pulse_file(pfy)
             if fx is None or fy is None:
-                sx, sy = _sample_pulses(use_pulses, ts)
+                if pulse_sampling == "ace_file":
+                    tf, sx, sy = _ace_file_samples(t_file, *_sample_pulses(use_pulses, t_file))
+                    if fx is None:
+                        tx = tf
+                    if fy is None:
+                        ty = tf
+                else:
+                    sx, sy = _sample_pulses(use_pulses, ts)
                 if fx is None:
                     fx = sx
                 if fy is None:
@@ -262,6 +288,9 @@ def system_ace_stream(t_start, t_end, *pulses, dt=0.01, phonons=False, t_mem=20.
         if rf_op is not None:
             if rf_file is not None:
                 tr, fr = read_pulse_file(rf_file)
+            elif pulse_sampling == "ace_file":
+                tr, fr = _ace_file_samples(t_file, np.asarray(pulse_list[0].get_frequency(t_file), dtype=complex)
+                                           * np.ones_like(t_file))
             else:
                 tr, fr = ts, np.asarray(pulse_list[0].get_frequency(ts), dtype=complex) * np.ones_like(ts)
             add_channel(rf_op, -0.5 * hbar, tr, fr)

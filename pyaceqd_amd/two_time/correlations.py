@@ -202,6 +202,166 @@ def tl_three_op_two_time(system, t_axis, *pulses, t_mem=10, opA="|1><0|_2", opB=
                      [mto, mto2], (A, B))
 
 
+def get_spectrum(g1, tau, dir="", plot=False):
+    """Spectrum under continuous-wave excitation from G1(tau) (correlations.py:322-380): the offset G1(tau_max) is
+    subtracted, G1 is continued to negative tau as conj(G1(-tau)), and S(omega) = Re FFT, fft-shifted, on the
+    energy axis 2 pi hbar fftfreq (meV). Returns (s, omega). plot=True writes the reference's three figures
+    (g1_tendsymm.png, spectrum_log.png, spectrum_nolog.png) into `dir` (matplotlib; plotting is not on the
+    propagation path)."""
+    from ..constants import hbar
+    g1 = np.array(g1, dtype=complex, copy=True)
+    tau = np.asarray(tau)
+    dtau = np.abs(tau[1] - tau[0])
+    g1 = g1 - g1[-1]
+    g1 = np.concatenate((np.conj(np.flip(g1[1:])), g1))
+    tau = np.concatenate((-np.flip(tau[1:]), tau))
+    s_omega = np.fft.fftshift(np.real(np.fft.fft(g1)))
+    fft_freqs = np.fft.fftshift(2 * np.pi * hbar * np.fft.fftfreq(len(g1), d=dtau))
+    if plot:
+        import matplotlib.pyplot as plt
+        for name, x, y, xl, lim in (("g1_tendsymm.png", tau, np.abs(g1), "Time (ps)", (-1, 1)),
+                                    ("spectrum_log.png", fft_freqs, np.log(np.abs(s_omega)), "Frequency (meV)",
+                                     (-3, 3)),
+                                    ("spectrum_nolog.png", fft_freqs, np.abs(s_omega), "Frequency (meV)", (-3, 3))):
+            plt.clf()
+            plt.plot(x, y)
+            plt.xlim(*lim)
+            plt.xlabel(xl)
+            plt.savefig(dir + name)
+    return s_omega, fft_freqs
+
+
+def _phonon_maps(system, pulses, t_mem, opA, opC, dt, rho0, options):
+    """first part of the two phonon-map functions (correlations.py:876-884, 1023-1031): dynamical maps of a
+    0 .. 4 t_mem run with C rho A applied at 1.2 t_mem, time-localised; the stationary map before the MTO, the
+    memory-time blocks before / after it, and the last time-local map"""
+    mto = {"operator": opC, "applyFrom": "_left", "applyBefore": "false", "time": 1.2 * t_mem}
+    mto2 = {"operator": opA, "applyFrom": "_right", "applyBefore": "false", "time": 1.2 * t_mem}
+    result, dm = system(0, 4 * t_mem, *pulses, dt=dt, rho0=rho0, multitime_op=[mto, mto2], calc_dynmap=True,
+                        **options)
+    _t = np.round(np.real(result[0]), 6)
+    dm_tl = calc_tl_dynmap_pseudo(dm, _t)
+    tl_map, dms_separated = extract_dms(dm_tl, _t, t_mem, [1.2 * t_mem])
+    return tl_map, np.array(dms_separated, dtype=complex), dm_tl[-1]
+
+
+def tl_three_op_two_time_phonons(system, t_axis, *pulses, t_mem=10, opA="|1><0|_2", opB="|1><1|_2",
+                                 opC="|0><1|_2", tau_max=500, dt=0.1, rho0=np.array([[1, 0], [0, 0]], dtype=complex),
+                                 options={"lindblad": True, "phonons": True}, debug=False, fortran_only=False):
+    """<A(t) B(t + tau) C(t)> with phonons from dynamical maps (correlations.py:866-1011).
+
+    t < t_mem: the memory-time block after the MTO comes from a dynamical-map run with the MTO at t itself; later
+    t use the block of the 1.2 t_mem run; the trunk uses the block before the MTO, then the stationary map; past
+    the block every row continues with the last time-local map. Same G as the reference. Its debugging side
+    effects are not reproduced: the rho_test reconstruction, the figures written to pyaceqd/tests/*.png and the
+    extra 0 .. 200 ps dynamical-map run at the hard-coded i_test = 9 (which makes the reference fail for fewer
+    than 10 t points and for dim != 2; this one does not)."""
+    if not t_axis[0] == 0:
+        raise ValueError("t_axis must start at 0.")
+    t_axis = np.round(t_axis, 6)
+    A, B, Cm = op_to_matrix(opA), op_to_matrix(opB), op_to_matrix(opC)
+    tl_map, dms_separated, tl_map2 = _phonon_maps(system, pulses, t_mem, opA, opC, dt, rho0, options)
+    n_tau = int(tau_max / dt)
+    tau = np.linspace(0, tau_max, n_tau + 1)
+    G = np.zeros((len(t_axis), len(tau)), dtype=complex)
+    dim = len(rho0[0])
+    t_mem_indices = np.where(t_axis < t_mem)[0]
+    dms_tauc = np.empty((len(t_mem_indices), *np.shape(dms_separated)), dtype=complex)
+    for i in t_mem_indices:
+        t = t_axis[i]
+        mto = {"operator": opC, "applyFrom": "_left", "applyBefore": "false", "time": t}
+        mto2 = {"operator": opA, "applyFrom": "_right", "applyBefore": "false", "time": t}
+        result, dm = system(0, t + t_mem + 10 * dt, *pulses, dt=dt, rho0=rho0, multitime_op=[mto, mto2],
+                            calc_dynmap=True, **options)
+        _t = np.round(result[0], 6)
+        _, _dms = extract_dms(calc_tl_dynmap_pseudo(dm, _t), _t, t_mem, [t])
+        dms_tauc[i] = _dms
+    n_tauc = len(dms_tauc[0, 0])
+    ABC = A @ B @ Cm
+    Bt = B.T.reshape(dim * dim)            # Tr(B R) = sum_ab B[b, a] R[a, b] over row-major vec(R)
+    X = np.empty((dim * dim, len(t_axis)), dtype=complex)
+    for i, t in enumerate(t_axis):
+        rho_t = np.asarray(rho0, dtype=complex).copy().reshape(dim ** 2)
+        n_steps = 0 if i == 0 else int(np.round(t / dt, 6)) + 1
+        for j in range(np.min([n_steps, n_tauc]) - 1):
+            rho_t = dms_separated[0, j] @ rho_t
+        for j in range(n_steps - n_tauc):
+            rho_t = tl_map @ rho_t
+        G[i, 0] = np.trace(ABC @ rho_t.reshape(dim, dim))
+        blk = dms_tauc[i, 1] if i < len(t_mem_indices) else dms_separated[1]
+        for j in range(n_tauc):
+            rho_t = blk[j] @ rho_t
+            G[i, j + 1] = Bt @ rho_t
+        X[:, i] = rho_t
+    rows = np.arange(len(t_axis))
+    for j in range(n_tau - n_tauc):
+        X = tl_map2 @ X
+        G[rows, n_tauc + j + 1] = Bt @ X
+    return t_axis, tau, G
+
+
+def tl_threeoptwotime_phonons_dm(system, t_axis, *pulses, t_mem=10, opA="|1><0|_2", opB="|1><1|_2", opC="|0><1|_2",
+                                 tau_max=500, dt=0.1, rho0=np.array([[1, 0], [0, 0]], dtype=complex),
+                                 options={"lindblad": True, "phonons": True}, debug=False, fortran_only=False):
+    """<A(t) B(t + tau) C(t)> with phonons (correlations.py:1013-1186): for t <= t_mem the full (not time-local)
+    dynamical maps E(t_k, 0) of a 0 .. t + t_mem run with the MTO at t give rho(t) = E(t, 0) rho0 and
+    rho(t + tau) = E(t + tau, 0) rho0 directly; later t and every tail past the maps as in
+    tl_three_op_two_time_phonons. Same G as the reference; its debugging side effects (rho_test, figures, the
+    i_test = 9 run) are not reproduced."""
+    if not t_axis[0] == 0:
+        raise ValueError("t_axis must start at 0.")
+    t_axis = np.round(t_axis, 6)
+    A, B, Cm = op_to_matrix(opA), op_to_matrix(opB), op_to_matrix(opC)
+    tl_map, dms_separated, tl_map2 = _phonon_maps(system, pulses, t_mem, opA, opC, dt, rho0, options)
+    n_tau = int(tau_max / dt)
+    tau = np.linspace(0, tau_max, n_tau + 1)
+    G = np.zeros((len(t_axis), len(tau)), dtype=complex)
+    dim = len(rho0[0])
+    t_mem_indices = np.where(t_axis <= t_mem)[0]
+    dms_tauc = []
+    for i in t_mem_indices:
+        t = t_axis[i]
+        mto = {"operator": opC, "applyFrom": "_left", "applyBefore": "false", "time": t}
+        mto2 = {"operator": opA, "applyFrom": "_right", "applyBefore": "false", "time": t}
+        _, dm = system(0, t + t_mem, *pulses, dt=dt, rho0=rho0, multitime_op=[mto, mto2], calc_dynmap=True,
+                       **options)
+        dms_tauc.append(dm.copy())
+    ABC = A @ B @ Cm
+    Bt = B.T.reshape(dim * dim)
+    r0 = np.asarray(rho0, dtype=complex).copy().reshape(dim ** 2)
+    for i in range(len(t_mem_indices)):
+        dm = dms_tauc[i]
+        n_steps = 0 if i == 0 else int(np.round(t_axis[i] / dt, 6))
+        rho_t = dm[n_steps - 1] @ r0 if n_steps > 0 else r0.copy()
+        G[i, 0] = np.trace(ABC @ rho_t.reshape(dim, dim))
+        rho_t_mto = rho_t.copy()
+        n_map = dm.shape[0] - n_steps
+        for j in range(n_map):
+            rho_t_mto = dm[j + n_steps] @ r0
+            G[i, j + 1] = Bt @ rho_t_mto
+        _tail_rows(G, i, rho_t_mto, tl_map2, n_map, n_tau - n_map, Bt)
+    tl_1, tl_2 = dms_separated[0], dms_separated[1]
+    for i in range(len(t_mem_indices), len(t_axis)):
+        rho_t = r0.copy()
+        n_steps = int(np.round(t_axis[i] / dt, 6))
+        for j in range(len(tl_1)):
+            rho_t = tl_1[j] @ rho_t
+        for j in range(n_steps - len(tl_1)):
+            rho_t = tl_map @ rho_t
+        G[i, 0] = np.trace(ABC @ rho_t.reshape(dim, dim))
+        for j in range(tl_2.shape[0]):
+            rho_t = tl_2[j] @ rho_t
+            G[i, j + 1] = Bt @ rho_t
+        _tail_rows(G, i, rho_t, tl_map2, tl_2.shape[0], n_tau - tl_2.shape[0], Bt)
+    return t_axis, tau, G
+
+
+def _tail_rows(G, i, x, tl_map2, col0, n, Bt):
+    for j in range(n):
+        x = tl_map2 @ x
+        G[i, col0 + j + 1] = Bt @ x
+
+
 def _tl_stationary_three_op(system, t_axis, pulses, t_mem, ops, tau_max, dt, rho0, options, mtos_dyn):
     """opt-in three-op form of the stationary-map branch (see tl_three_op_two_time)"""
     A, B, Cm = ops

@@ -309,7 +309,7 @@ def gen_correlations():
         for tag, fn, kw in (("tl2", R.tl_two_op_two_time, {}),
                             ("tl3", R.tl_three_op_two_time, {"opC": "|0><1|_2"})):
             for use_dm, fo in ((False, False), (True, False), (True, True)):
-                t1, t2, G = fn(fake_system_dm, t_axis, p, t_mem=1.0, tau_max=2.0, dt=0.1, rho0=rho2,
+                t1, t2, G = fn(fake_system_dm, t_axis, p, t_mem=1.0, tau_max=50.0, dt=0.1, rho0=rho2, opB="|0><0|_2",
                                options=opts(), use_dm=use_dm, fortran_only=fo, **kw)
                 out[f"{tag}_dm{int(use_dm)}_f{int(fo)}_G"] = G
                 out[f"{tag}_t2"] = t2
@@ -323,6 +323,48 @@ def gen_correlations():
                                                options=opts(fake_dim=4), use_dm=use_dm, fortran_only=fo)
             out[f"tl3d4_dm{int(use_dm)}_f{int(fo)}_G"] = G
     np.savez_compressed(os.path.join(HERE, "pyref_correlations.npz"), **out)
+
+
+def gen_correlations_phonons():
+    """The rest of two_time/correlations.py: the REFERENCE get_spectrum (:322-380) on an analytic G1 (two damped
+    lines plus an offset) and the two phonon dynamical-map functions tl_three_op_two_time_phonons (:866-1011) and
+    tl_threeoptwotime_phonons_dm (:1013-1186) on tests/fake_system.py's calc_dynmap model (dim 2: their debugging
+    code is written for 2x2, needs >= 10 t points and t_axis[-1] + tau_max >= 49.9 ps). They save figures to the relative path pyaceqd/tests/, so
+    they run inside a scratch directory that has one."""
+    import io
+    import contextlib
+    import tempfile
+    import warnings
+    warnings.simplefilter("ignore")
+    R = _ref_correlations()
+    import matplotlib
+    matplotlib.use("Agg")
+    from pyaceqd.pulses import ChirpedPulse  # noqa: E402
+    from tests.fake_system import fake_system_dm  # noqa: E402
+    tau = np.round(0.05 * np.arange(801), 6)
+    g1 = (0.7 * np.exp(-0.3 * tau - 1j * 1.1 * tau) + 0.3 * np.exp(-0.8 * tau + 1j * 0.4 * tau)
+          + 0.01 * (1 + 0.5j))
+    s, om = R.get_spectrum(g1, tau)
+    out = {"sp_g1": g1, "sp_tau": tau, "sp_s": s, "sp_omega": om}
+    p = ChirpedPulse(tau_0=1.0, e_start=0, e0=1.5, t0=2)
+    rho2 = np.array([[0.8, 0.1 - 0.05j], [0.1 + 0.05j, 0.2]], dtype=complex)
+    t_axis = np.round(np.arange(12) * 0.2, 6)
+    out["ph_t_axis"] = t_axis
+    here = os.getcwd()
+    with tempfile.TemporaryDirectory() as d:
+        os.makedirs(os.path.join(d, "pyaceqd", "tests"))
+        os.chdir(d)
+        try:
+            with contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
+                for tag, fn in (("ph", R.tl_three_op_two_time_phonons), ("phdm", R.tl_threeoptwotime_phonons_dm)):
+                    _, tau2, G = fn(fake_system_dm, t_axis, p, t_mem=1.0, tau_max=50.0, dt=0.1, rho0=rho2, opB="|0><0|_2",
+                                    options={"lindblad": True, "phonons": True,
+                                             "output_ops": ["|0><0|_2", "|1><1|_2"]})
+                    out[f"{tag}_tau"] = tau2
+                    out[f"{tag}_G"] = G
+        finally:
+            os.chdir(here)
+    np.savez_compressed(os.path.join(HERE, "pyref_correlations_phonons.npz"), **out)
 
 
 def gen_twotime_anchor():
@@ -566,6 +608,7 @@ if __name__ == "__main__":
     gen_fortran()
     gen_pyref()
     gen_correlations()
+    gen_correlations_phonons()
     gen_twotime_anchor()
     gen_polent()
     gen_purity()

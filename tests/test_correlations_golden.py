@@ -174,3 +174,43 @@ def test_trajectory_sweep_matches_reference_map_formula_cpu(anchor, monkeypatch)
 def test_trajectory_sweep_matches_reference_map_formula_gpu(anchor):
     """the HIP sweep (MTOs at t1 in the kernel) vs the reference's map-based G2 / G1 on the same biexciton"""
     _check_anchor(anchor, *_anchor_runs(anchor))
+
+
+# ------------------------------------------------------------------------------------------- spectrum, phonon maps
+@pytest.fixture(scope="module")
+def zph(golden_dir):
+    return np.load(os.path.join(golden_dir, "pyref_correlations_phonons.npz"))
+
+
+def test_get_spectrum_matches_reference(zph):
+    """reference get_spectrum (correlations.py:322-380) on an analytic two-line G1 with an offset"""
+    s, om = corr.get_spectrum(zph["sp_g1"], zph["sp_tau"])
+    close(om, zph["sp_omega"])
+    close(s, zph["sp_s"])
+
+
+def _phonon_map_call(fn, zph):
+    return fn(fake_system_dm, zph["ph_t_axis"], _p(), t_mem=1.0, tau_max=50.0, dt=0.1,
+              rho0=np.array([[0.8, 0.1 - 0.05j], [0.1 + 0.05j, 0.2]], dtype=complex), opB="|0><0|_2",
+              options={"lindblad": True, "phonons": True, "output_ops": ["|0><0|_2", "|1><1|_2"]})
+
+
+@pytest.mark.parametrize("name,tag", [("tl_three_op_two_time_phonons", "ph"),
+                                      ("tl_threeoptwotime_phonons_dm", "phdm")])
+def test_phonon_map_correlations_match_reference(monkeypatch, zph, name, tag):
+    """reference tl_three_op_two_time_phonons (:866-1011) / tl_threeoptwotime_phonons_dm (:1013-1186) on the
+    calc_dynmap fake model: t < t_mem rows from per-t dynamical-map runs, later rows from the 1.2 t_mem run, tails
+    on the last time-local map (the GPU batched pinv replaced by the oracle here; tests/test_gpu_parity.py runs it)"""
+    _oracle_kernels(monkeypatch)
+    t, tau, G = _phonon_map_call(getattr(corr, name), zph)
+    close(tau, zph[f"{tag}_tau"])
+    close(G, zph[f"{tag}_G"], 1e-11)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,tag", [("tl_three_op_two_time_phonons", "ph"),
+                                      ("tl_threeoptwotime_phonons_dm", "phdm")])
+def test_phonon_map_correlations_match_reference_gpu(zph, name, tag):
+    """the same with the time-local maps from the GPU batched pinv (tlmap.hip)"""
+    t, tau, G = _phonon_map_call(getattr(corr, name), zph)
+    close(G, zph[f"{tag}_G"], 1e-10)

@@ -160,6 +160,30 @@ def test_trunk_prepass_split_timeout_falls_back(monkeypatch):
         assert rel(a, b) < 1e-11, rel(a, b)
 
 
+@pytest.mark.parametrize("spin", ["default", "0"])
+def test_trunk_prepass_in_consecutive_launches(monkeypatch, spin):
+    """more six-level trunks than the device holds as co-resident split groups (8 trunks x 36 workgroups on 256
+    CUs: 7 + 1 launches, pqd_host.cpp tk_chunk; the C5 tomography scan's shape). With PQD_SPLIT_SPIN=0 every wait
+    for a peer times out and the pre-pass falls back to batched workgroups"""
+    N, chi, n_sys = 6, 16, 8
+    monkeypatch.setenv("PQD_TRUNK", "1")
+    if spin == "0":
+        monkeypatch.setenv("PQD_SPLIT_SPIN", "0")
+    systems = [H.random_system(N, n_steps=30, seed=70 + k)[0] for k in range(n_sys)]
+    grid = Grid(0.0, 0.1, 30)
+    tr = g2_reuse_shape(30, 40, N, n_sys=n_sys, seed=11)
+    pt = ptmod.random_pt(N, chi, D=9, n_slices=8, seed=12, eps=0.1)
+    ops = [H.ketbra(N, 1, 1), H.ketbra(N, 5, 0)]
+    rho0 = H.random_rho(N)
+    plan = engine.Plan(systems, grid, rho0, ops, tr, pt=pt)
+    plan.execute()
+    got = plan.download()
+    assert plan.info()[2] == (1 if spin == "0" else 0)
+    ref = oracle.propagate(systems, grid, rho0, ops, tr, pt=pt, nthreads=8)
+    for a, b in zip(got, ref):
+        assert rel(a, b) < 1e-11, rel(a, b)
+
+
 def test_trunk_prepass_halves_g2_reuse_steps(monkeypatch):
     N, chi, n_steps, n_t1 = 4, 16, 400, 256
     monkeypatch.setenv("PQD_TRUNK", "1")

@@ -1,0 +1,246 @@
+"""The five BASELINE.json configurations, each run through the HIP path at the size the
+configuration names, with the checks that size allows. GPU only.
+
+  config 1  "two_level_system Rabi, no phonons, 1000 steps"      tls(0, 100, ChirpedPulse(tau_0=3, e_start=0, e0=1,
+            t0=20), dt=0.1, lindblad=True) through the drop-in driver vs the same lowering on the CPU oracle, and the
+            Rabi population against a direct Lindblad master-equation integration (scipy, independent of both)
+  config 2  "two_level_system with phonon PT, bond-dim 32"        2,048-point pulse-area scan x 10,000 steps, chi=32,
+            on the register-resident quad kernel (pt_quad.hip): vs the batched kernel (PQD_QUAD=0) to 1e-11, vs the
+            oracle on three full-length trajectories, and a structured PT (bond channel 0 decoupled) == bare dynamics
+            with the trace preserved to 1e-10 over every step
+  config 3  "four_level_system biexciton cascade, bond-dim 64"    tests/test_gpu_parity.py::test_c3_full_size_invariants
+            (10,000 steps, chi=64) and ::test_sweep_pt_split_full_c3_single_run; here the single run vs the oracle
+  config 4  "two_time G2(t, tau) sweep, 256 tau-points"           256 t1 trajectories x 10,000 tau-steps, chi=64,
+            biexciton (bench.build_workload): an unstructured PT vs the oracle on a 16-point sub-grid at full length,
+            and the structured PT == bare dynamics over the whole grid; one rank's 32-point shard equals its block
+            of the whole-grid run bit for bit (the shard each of 8 GPUs runs)
+  config 5  "six_level_system + pol_entanglement tomography scan" densitymatrix_reuse_scan (three launches for the
+            grid) at chi=64 with the class's t1 grid and its 6/8/6 output operators vs each point run on its own, and
+            vs the oracle at reduced tend
+
+The reference states no numbers for these (ACE is absent): every comparison is against the CPU
+oracle (oracle/pqd_oracle.c), a second HIP kernel, or a property the physics fixes. Tolerances: 1e-11 relative
+between two GPU kernels, 1e-10 against the oracle over 10,000 steps (summation-order differences of a few 1e-16 per
+step), far below the north star's 1e-8."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+from pyaceqd_amd import engine, opgrammar, pt as ptmod
+from pyaceqd_amd.engine import Trajectories
+from tests.test_gpu_parity import _oracle_patch, cmp_lists, rel
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _subset(tr, ids):
+    """trajectories `ids` of tr as a Trajectories of their own (MTOs and systems remapped)"""
+    ids = [int(i) for i in ids]
+    remap = {t: k for k, t in enumerate(ids)}
+    mt = [type(m)(remap[m.traj], m.step, m.before, m.kind, m.op) for m in tr.mtos if m.traj in remap]
+    sysidx = None if tr.system is None else np.asarray(tr.system)[ids]
+    return Trajectories(np.asarray(tr.out_begin)[ids], np.asarray(tr.out_end)[ids], mt, system=sysidx)
+
+
+def _configs():
+    sys.path.insert(0, os.path.join(HERE, "scripts"))
+    import bench_configs
+    return bench_configs
+
+
+# ------------------------------------------------------------------------------------------------ config 1
+def test_config1_tls_rabi_1000_steps(monkeypatch):
+    from scipy.integrate import solve_ivp
+    from pyaceqd_amd.constants import hbar
+    from pyaceqd_amd.pulses import ChirpedPulse
+    from pyaceqd_amd.two_level_system.tls import tls
+    p = ChirpedPulse(tau_0=3, e_start=0, e0=1, t0=20)
+    a = tls(0, 100, p, dt=0.1, lindblad=True)
+    assert a.shape == (5, 1001)
+    assert np.max(np.abs(a[1] + a[2] - 1)) < 1e-12          # populations sum to one
+    _oracle_patch(monkeypatch)
+    b = tls(0, 100, p, dt=0.1, lindblad=True)
+    assert np.max(np.abs(a - b)) < 1e-12
+    # Lindblad master equation of the same model (tls.py:24-29 strings: H = -pi hbar/2 (f |1><0| + h.c.), decay
+    # |0><1| at 1/100 per ps), integrated directly with an adaptive RK; the engine's symmetric Trotter steps at
+    # dt = 0.1 differ by O(dt^2)
+    g = 1 / 100
+    s = np.array([[0, 1], [0, 0]], complex)      # |0><1|
+
+    def rhs(t, y):
+        r = y.reshape(2, 2)
+        f = complex(p.get_total(np.array([t]))[0])
+        X = -0.5 * np.pi * hbar * np.array([[0, 0], [1, 0]], complex)
+        H = f * X + np.conj(f) * X.conj().T
+        d = -1j / hbar * (H @ r - r @ H) + g * (s @ r @ s.conj().T - 0.5 * (s.conj().T @ s @ r + r @ s.conj().T @ s))
+        return d.ravel()
+    sol = solve_ivp(rhs, (0, 100), np.array([1, 0, 0, 0], complex), t_eval=[25.0, 40.0, 100.0], rtol=1e-11,
+                    atol=1e-13, method="DOP853")
+    exc = sol.y[3].real                            # rho_11 (measured: 0.95223, 0.82790, 0.45436; engine within 1e-6)
+    assert np.max(np.abs(a[2][[250, 400, 1000]].real - exc)) < 1e-5
+    assert exc[0] > 0.9                            # a pi pulse: the dot is inverted, then decays
+
+
+# ------------------------------------------------------------------------------------------------ config 2
+def _c2(structured):
+    bc = _configs()
+    N, systems, grid, pt, rho0, ops, tr = bc.workload(**bc.CONFIGS["c2"])
+    assert (N, len(systems), tr.n_traj, grid.n_steps, pt.chi) == (2, 2048, 2048, 10000, 32)
+    if not structured:
+        pt = ptmod.synthetic_pt(opgrammar.to_matrix("1.000*|1><1|_2", 2), chi=32, n_init=410, n_rep=1, seed=99,
+                                eps=0.05, dt=0.1, structured=False)
+    return systems, grid, pt, rho0, ops + [np.eye(2)], tr
+
+
+def _plan_run(systems, grid, rho0, ops, tr, pt):
+    plan = engine.Plan(systems, grid, rho0, ops, tr, pt=pt)
+    plan.execute()
+    return plan.download(), plan.info()[0]
+
+
+def test_config2_tls_chi32_full_scan_quad_vs_batched_and_oracle(monkeypatch):
+    monkeypatch.setenv("PQD_SPLIT", "0")
+    systems, grid, pt, rho0, ops, tr = _c2(structured=False)
+    a, path = _plan_run(systems, grid, rho0, ops, tr, pt)
+    assert path == "register-resident TLS quads"
+    ids = [0, 1023, 2047]
+    sub = _subset(tr, ids)
+    ref = oracle.propagate([systems[i] for i in ids], grid, rho0, ops,
+                           Trajectories(sub.out_begin, sub.out_end, sub.mtos, system=np.arange(3)), pt=pt, nthreads=8)
+    cmp_lists([a[i] for i in ids], ref, 1e-10)
+    monkeypatch.setenv("PQD_QUAD", "0")
+    b, path = _plan_run(systems, grid, rho0, ops, tr, pt)
+    assert path == "batched lock-step sweep"
+    cmp_lists(a, b, 1e-11)
+    assert max(float(np.max(np.abs(x[:, 0]))) for x in a) > 0.1   # the scan drives the dots
+
+
+def test_config2_tls_chi32_full_scan_structured_pt_is_bare_dynamics(monkeypatch):
+    monkeypatch.setenv("PQD_SPLIT", "0")
+    systems, grid, pt, rho0, ops, tr = _c2(structured=True)
+    a, path = _plan_run(systems, grid, rho0, ops, tr, pt)
+    assert path == "register-resident TLS quads"
+    b, _ = _plan_run(systems, grid, rho0, ops, tr, None)
+    for x, y in zip(a, b):
+        assert np.max(np.abs(x - y)) < 1e-10
+        assert np.max(np.abs(x[:, -1] - 1)) < 1e-10           # trace preserved at every step
+
+
+# ------------------------------------------------------------------------------------------------ config 3
+def test_config3_biexciton_chi64_single_run_vs_oracle():
+    """the reference's single-run case: one biexciton trajectory, chi = 64, 10,000 steps (split groups, §4.6)"""
+    bc = _configs()
+    N, sysd, grid, pt, rho0, ops, tr = bc.workload(**bc.CONFIGS["c3one"])
+    pt = ptmod.synthetic_pt(opgrammar.to_matrix("1*(|1><1|_4 + |2><2|_4) + 2*|3><3|_4", 4), chi=64, n_init=410,
+                            n_rep=1, seed=5, eps=0.05, dt=0.1, structured=False)
+    plan = engine.Plan(sysd, grid, rho0, ops, tr, pt=pt)
+    plan.execute()
+    got = plan.download()
+    assert got[0].shape == (10001, 2)
+    cmp_lists(got, oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-10)
+
+
+# ------------------------------------------------------------------------------------------------ config 4
+def _c4(structured):
+    import bench
+    sysd, grid, pt, rho0, ops, tr = bench.build_workload(256, 10000, 64, scan=1)
+    if not structured:
+        pt = ptmod.synthetic_pt(opgrammar.to_matrix("1*(|1><1|_4 + |2><2|_4) + 2*|3><3|_4", 4), chi=64, n_init=410,
+                                n_rep=1, seed=77, eps=0.05, dt=0.1, structured=False)
+    assert tr.n_traj == 256 and int(tr.out_end[-1] - tr.out_begin[-1]) == 10000
+    return sysd, grid, pt, rho0, ops, tr
+
+
+def test_config4_g2_sweep_256_t1_full_length_vs_oracle_subgrid():
+    sysd, grid, pt, rho0, ops, tr = _c4(structured=False)
+    plan = engine.Plan(sysd, grid, rho0, ops, tr, pt=pt)
+    plan.execute()
+    got = plan.download()
+    assert got[0].shape == (10001, 2)
+    ids = np.arange(0, 256, 16)
+    ref = oracle.propagate(sysd, grid, rho0, ops, _subset(tr, ids), pt=pt, nthreads=16)
+    cmp_lists([got[i] for i in ids], ref, 1e-10)
+    # G2(t1, 0) = <A B C>(t1) lives in output 1 at the first row; the sweep is not trivially zero
+    assert max(abs(g[0, 1]) for g in got) > 0
+
+
+def test_config4_g2_sweep_256_t1_structured_pt_is_bare_and_shards_are_exact():
+    sysd, grid, pt, rho0, ops, tr = _c4(structured=True)
+    a = engine.propagate(sysd, grid, rho0, ops, tr, pt=pt)
+    b = engine.propagate(sysd, grid, rho0, ops, tr)
+    for x, y in zip(a, b):
+        assert np.max(np.abs(x - y)) < 1e-10
+    # one GPU's shard of the 8-GPU split (32 t1 points per GPU) as a launch of its own
+    from pyaceqd_amd import scan as scanmod
+    import bench
+    for rank in (0, 7):
+        lo, hi = scanmod.shard_range(256, rank, 8)
+        s2, g2, p2, r2, o2, t2 = bench.build_workload(hi - lo, 10000, 64, scan=1, t1_offset=lo)
+        part = engine.propagate(s2, grid, r2, o2, t2, pt=pt)
+        for k in range(hi - lo):
+            assert np.array_equal(part[k], a[lo + k]) or rel(part[k], a[lo + k]) < 1e-13
+
+
+# ------------------------------------------------------------------------------------------------ config 5
+SX, SY = "|0><1|_6 + |1><5|_6", "|0><2|_6 + |2><5|_6"
+SXD, SYD = "|1><0|_6 + |5><1|_6", "|2><0|_6 + |5><2|_6"
+
+
+def _c5_insts(tend, tmp_path, e0s=(3.0, 5.5), bxs=(0.0, 2.0), t0=3.0, t0b=6.0, dt_small=None):
+    from pyaceqd_amd.pol_entanglement.G2 import PolarizatzionEntanglement
+    from pyaceqd_amd.pulses import ChirpedPulse
+    from pyaceqd_amd.six_level_system.linear import energies_linear, sixls_linear, sixls_ops
+    E_X, _, _, _, E_B = energies_linear(delta_B=4)
+    pt = ptmod.synthetic_pt(opgrammar.to_matrix(sixls_ops()[1], 6), chi=64, n_init=410, n_rep=1, seed=5, eps=0.05,
+                            dt=0.1, dictionary=True, structured=False)
+    insts, kws = [], []
+    for e0 in e0s:
+        for bx in bxs:
+            p1 = ChirpedPulse(tau_0=2.7, e_start=E_X, alpha=40, e0=e0, t0=t0)
+            p2 = ChirpedPulse(tau_0=2.7, e_start=E_B - E_X, alpha=40, e0=4.06, t0=t0b)
+            opts = {"lindblad": True, "gamma_e": 1 / 100, "phonons": True, "pt_file": pt,
+                    "temp_dir": str(tmp_path) + "/"}
+            kw = dict(regular_grid=True, dt_small=dt_small) if dt_small else {}
+            insts.append(PolarizatzionEntanglement(sixls_linear, SX, SY, SXD, SYD, p1, p2, dt=0.1, tend=tend,
+                                                   options=opts, **kw))
+            kws.append({"bx": bx})
+    return insts, kws
+
+
+def _c5_per_point(insts, kws):
+    from functools import partial
+    from pyaceqd_amd.six_level_system.linear import sixls_linear
+    out = []
+    for inst, kw in zip(insts, kws):
+        inst.system = partial(sixls_linear, **kw)
+        out.append(inst.calc_densitymatrix_reuse(return_rho=True))
+    return out
+
+
+def test_config5_tomography_scan_chi64_vs_per_point_runs(tmp_path):
+    """chi = 64 dictionary PT, the class's own (non-regular) t1 grid, tend 60 ps: 2 e0 x 2 bx points"""
+    from pyaceqd_amd.pol_entanglement.G2 import densitymatrix_reuse_scan
+    insts, kws = _c5_insts(60.0, tmp_path, t0=10.0, t0b=30.0)
+    got = densitymatrix_reuse_scan(insts, kws, return_rho=True)
+    assert len(insts[0].t1) > 100
+    ref = _c5_per_point(*_c5_insts(60.0, tmp_path, t0=10.0, t0b=30.0))
+    for (cg, rg), (cr, rr) in zip(got, ref):
+        assert rg.shape == (4, 4)
+        assert np.max(np.abs(rg - rr)) <= 1e-11 * np.max(np.abs(rr))
+        assert abs(cg - cr) < 1e-9
+    assert np.max(np.abs(got[0][1] - got[1][1])) > 1e-6 * np.max(np.abs(got[0][1]))   # bx matters
+
+
+def test_config5_tomography_scan_chi64_vs_oracle(monkeypatch, tmp_path):
+    from pyaceqd_amd.pol_entanglement.G2 import densitymatrix_reuse_scan
+    insts, kws = _c5_insts(12.0, tmp_path, dt_small=1.0)
+    got = densitymatrix_reuse_scan(insts, kws, return_rho=True)
+    _oracle_patch(monkeypatch)
+    ref = _c5_per_point(*_c5_insts(12.0, tmp_path, dt_small=1.0))
+    for (cg, rg), (cr, rr) in zip(got, ref):
+        assert np.max(np.abs(rg - rr)) <= 1e-10 * np.max(np.abs(rr))
+        assert abs(cg - cr) < 1e-8

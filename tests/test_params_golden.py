@@ -127,6 +127,30 @@ def test_model_lowering_matches_reference_param_file(params, name, monkeypatch):
         np.testing.assert_allclose(m.op, M(s), atol=0)
 
 
+@pytest.mark.parametrize("name", ["tls", "biexciton", "sixls"])
+def test_ace_file_pulse_sampling_reads_what_the_reference_writes(params, name, monkeypatch):
+    """pulse_sampling="ace_file": the engine's channel samples ARE the %.8f pulse files the reference writes for
+    ACE (general_system.py:55-71, 213), bit for bit, on the file's own grid (t_start, dt); between samples the
+    engine interpolates linearly and holds past t_end - dt, as for an explicit pulse_file_x/_y"""
+    g = params[name]
+    rec = _parse(g["param"])
+    kw = dict(g["kwargs"])
+    p1 = ChirpedPulse(tau_0=1.0, e_start=0.2, e0=1.3, t0=2.0, alpha=5.0, phase=0.3)
+    p2 = ChirpedPulse(tau_0=0.8, e_start=-1.0, e0=0.7, t0=3.0, polar_x=0.6)
+    got = _capture(monkeypatch)
+    _model(name)(0, 4, p1, p2, suffix="g", pulse_sampling="ace_file", **kw)
+    sysd = got["system"]
+    assert len(sysd.channels) == len(rec["pulse"])
+    for (X, f), (tok, s) in zip(sysd.channels, rec["pulse"]):
+        d = np.loadtxt(g["pulse_files"][tok].splitlines())
+        assert len(f) == len(d)
+        np.testing.assert_array_equal(np.asarray(f).real, d[:, 1])
+        np.testing.assert_array_equal(np.asarray(f).imag, d[:, 2])
+        assert sysd.sample_t0 == d[0, 0] and sysd.sample_dt == d[1, 0] - d[0, 0]
+    with pytest.raises(ValueError, match="pulse_sampling"):
+        _model(name)(0, 4, p1, suffix="g", pulse_sampling="files", **kw)
+
+
 def test_single_projector_matches_reference_op_to_matrix():
     """tools.op_to_matrix (reference tools.py:260-304: |n><m|_d only) for every projector of d = 2..6"""
     from pyaceqd_amd.tools import op_to_matrix
