@@ -11,6 +11,8 @@
  *                                   one launch.
  *   pqd_pt_create                   replaces `add_PT <file>` + the PT files ACE writes
  *                                   (general_system.py:146-197, 236); device-resident, shared per context.
+ *   pqd_ace_pt_shape / _read        read ACE's own PT files (general_system.py:153-157, 194-197) under a
+ *                                   stated layout assumption (ACE_PTB_V0)
  *   pqd_free_propagators            exposes the free propagator ACEutils.FreePropagator.update(t,dt).M
  *                                   (general_system.py:324-327, `get_M_t`).
  *   pqd_propagate_tau               f2py propagate_tau_module.propagate_tau   (two_time/propagate_tau.f90:3)
@@ -109,6 +111,21 @@ int pqd_ctx_synchronize(pqd_ctx* ctx);
 
 int pqd_pt_create(pqd_ctx* ctx, int32_t dim, const pqd_pt_desc* desc, pqd_pt** out);
 void pqd_pt_destroy(pqd_pt* pt);
+
+/* Reading the PT files ACE writes with `write_PT <name>`: <name>_initial, <name>_initial_0, <name>_repeated,
+ * <name>_repeated_0 (reference general_system.py:146-157, 190, 194-197; detection :153-156). ACE's layout is
+ * undocumented offline; the reader implements ONE stated assumption, "ACE_PTB_V0" (csrc/ace_pt.cpp header,
+ * INTEGRATION.md), and returns PQD_ERR_UNSUPPORTED, naming the file and the mismatch, for anything else
+ * (PQD_ERR_ARG when a file is missing). Host-only, no context. pqd_ace_pt_shape sizes the buffers;
+ * pqd_ace_pt_read fills a pqd_pt_desc-shaped set of caller buffers (Q: n_slices*D*chi*chi, closure:
+ * n_slices*chi, closure0/bond0: chi, gmap: dim*dim) with slices [0, n_init) from _initial and slice n_init (the
+ * repeated slice) from _repeated; smaller bonds are zero-padded to chi. */
+typedef struct {
+    int32_t n_init, n_slices, chi, D;
+} pqd_ace_pt_dims;
+int pqd_ace_pt_shape(const char* name, int32_t dim, pqd_ace_pt_dims* shape);
+int pqd_ace_pt_read(const char* name, int32_t dim, const pqd_ace_pt_dims* shape, pqd_c128* Q, pqd_c128* closure,
+                    pqd_c128* closure0, pqd_c128* bond0, int32_t* gmap);
 
 /* M_out: 2*n_steps matrices (N^2 x N^2, row-major): [2n] first half step, [2n+1] second. */
 int pqd_free_propagators(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* grid, pqd_c128* M_out);

@@ -47,6 +47,10 @@ class pqd_pt_desc(C.Structure):
                 ("closure", P_C128), ("closure0", P_C128), ("bond0", P_C128), ("gmap", P_I32)]
 
 
+class pqd_ace_pt_dims(C.Structure):
+    _fields_ = [("n_init", C.c_int32), ("n_slices", C.c_int32), ("chi", C.c_int32), ("D", C.c_int32)]
+
+
 class pqd_traj(C.Structure):
     _fields_ = [("n_traj", C.c_int32), ("out_begin", P_I32), ("out_end", P_I32), ("out_offset", P_I64),
                 ("n_mto", C.c_int32), ("mto_traj", P_I32), ("mto_step", P_I32), ("mto_before", P_I32),
@@ -64,6 +68,9 @@ _SIGS = {
     "pqd_ctx_synchronize": ([C.c_void_p], C.c_int),
     "pqd_pt_create": ([C.c_void_p, C.c_int32, C.POINTER(pqd_pt_desc), C.POINTER(C.c_void_p)], C.c_int),
     "pqd_pt_destroy": ([C.c_void_p], None),
+    "pqd_ace_pt_shape": ([C.c_char_p, C.c_int32, C.POINTER(pqd_ace_pt_dims)], C.c_int),
+    "pqd_ace_pt_read": ([C.c_char_p, C.c_int32, C.POINTER(pqd_ace_pt_dims), P_C128, P_C128, P_C128, P_C128, P_I32],
+                        C.c_int),
     "pqd_free_propagators": ([C.c_void_p, C.POINTER(pqd_system), C.POINTER(pqd_grid), P_C128], C.c_int),
     "pqd_propagate": ([C.c_void_p, C.POINTER(pqd_system), C.POINTER(pqd_grid), C.c_void_p, P_I32, P_C128,
                        C.c_int32, P_C128, C.POINTER(pqd_traj), P_C128, C.c_int64], C.c_int),

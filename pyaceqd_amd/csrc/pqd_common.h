@@ -220,3 +220,6 @@ bool quad_supported(int N2, int CHI);
 // ncg: 4-column groups per wave, 4 (strips of 16 columns, one wave per SIMD) or 2 (strips of 8, two waves per SIMD)
 int quad_qpw(int CHI, int qpw, int ncg);  // quads per workgroup launch_quad instantiates
 hipError_t launch_quad(int CHI, int n_quads, int qpw, int ncg, const SweepParams& p, hipStream_t s);
+
+// thread-local last error shared by the host translation units (pqd_host.cpp owns it); returns code
+extern "C" int pqd_fail_msg(int code, const char* msg);

@@ -1201,6 +1201,8 @@ int pqd_propagate_table(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems, 
     return rc;
 }
 
+int pqd_fail_msg(int code, const char* msg) { return fail(code, "%s", msg); }
+
 // =================================================================================================
 // map-chain sweeps
 // =================================================================================================

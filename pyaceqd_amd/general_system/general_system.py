@@ -134,6 +134,12 @@ def _resolve_pt(pt_file, boson_mat, *, dt, t_mem, ae, temperature, threshold, fa
                                       use_infinite=use_infinite)
         pt_file = os.path.join(temp_dir, pt_file) if temp_dir else pt_file
     pt_file = str(pt_file)
+    from .. import ace_pt
+    if ace_pt.ace_pt_exists(pt_file) and J_to_file is None:
+        # ACE's own files (detected as the reference does, :153-156), read under layout ACE_PTB_V0 (ace_pt.py)
+        if verbose:
+            print("using pt_file " + pt_file)
+        return ace_pt.read_ace_pt(pt_file, boson_mat.shape[0], dt=dt)
     for cand in (pt_file, pt_file + ".npz"):
         if os.path.isfile(cand) and J_to_file is None:
             if verbose:
