@@ -8,6 +8,7 @@
 // 64 / N2 trajectories, lane (traj, r) owns row r of that trajectory's Liouville vector.
 // One wave per workgroup, so every __syncthreads() is a single s_barrier.
 #include "pqd_common.h"
+#include <algorithm>
 #include <cstdlib>
 
 namespace {
@@ -226,6 +227,266 @@ __global__ __launch_bounds__(64) void mc_tau_pipe_kernel(MapChainParams p) {
         if (k + sl <= ncol) step(sl, k + sl);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Blocked sweep for calc_onetime_parallel (mode 0). Every trajectory i runs along the same map sequence E[q]
+// (q = map index, 0-based): the trunk applies E[0 .. p_i - 1], the tau sweep E[p_i .. p_i + n_tau - 1]
+// (p_i = j_i - 1, propagate_tau.f90:144-181). The sequence is cut into blocks of L positions and, per block c,
+// the products R_c(q) = E[q] ... E[cL] are formed once (mcb_prefix_kernel, blocks in parallel) and kept as
+// U[q] = w^T R_c(q) (the trace functional) and Rend[c] = R_c(last). A trajectory then needs only a short
+// dependent chain: the map-by-map steps up to its first block boundary (outputs written directly) and one
+// Rend matvec per later block (mcb_tau_kernel); every later output is the dot U[q] . X_i[c]
+// (mcb_out_kernel, all (i, tau) in parallel). Same products as the reference's chain, associated per block:
+// results agree to rounding (the Fortran goldens and the pipelined kernel, PQD_MC_BLOCKED=0).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ double2 trace_weight(const MapChainParams& p, int r) {
+    // Tr(opB R) over the column-major view of R (propagate_tau.f90:176): lane r = b + a dim gets opB(a, b)
+    const int a = r / p.dim, b = r % p.dim;
+    return p.opB[a + b * p.dim];
+}
+
+template <int N2>
+__global__ __launch_bounds__(256) void mcb_prefix_kernel(MapChainParams p) {
+    constexpr int M2 = N2 * N2;
+    constexpr int PER = (M2 + 255) / 256;
+    __shared__ double2 R[2][M2];
+    __shared__ double2 E[M2];
+    __shared__ double2 w[N2];
+    const int tid = threadIdx.x, c = blockIdx.x;
+    const int q0 = c * p.L, q1 = min(q0 + p.L, p.Q);
+    if (tid < N2) w[tid] = trace_weight(p, tid);
+    double2 nx[PER];
+    auto fetch = [&](int q) {
+        const double2* A = p.dmA + (size_t)q * M2;
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int e = tid + 256 * u;
+            nx[u] = (e < M2) ? A[e] : c_zero();
+        }
+    };
+    fetch(q0);
+    int cur = 0;
+    for (int q = q0; q < q1; ++q) {
+        __syncthreads();  // the previous product and U read R / E
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int e = tid + 256 * u;
+            if (e < M2) E[e] = nx[u];
+        }
+        if (q + 1 < q1) fetch(q + 1);
+        __syncthreads();
+        if (q == q0) {
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const int e = tid + 256 * u;
+                if (e < M2) R[cur][e] = E[e];
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const int e = tid + 256 * u;
+                if (e < M2) {
+                    const int rr = e % N2, cc = e / N2;
+                    double2 acc = c_zero();
+#pragma unroll 4
+                    for (int k = 0; k < N2; ++k) c_fma(acc, E[rr + k * N2], R[cur][k + cc * N2]);
+                    R[cur ^ 1][e] = acc;
+                }
+            }
+            cur ^= 1;
+        }
+        __syncthreads();
+        if (tid < N2) {  // U[q][col] = sum_k w[k] R(k, col)
+            double2 acc = c_zero();
+            for (int k = 0; k < N2; ++k) c_fma(acc, w[k], R[cur][k + tid * N2]);
+            p.U[(size_t)q * N2 + tid] = acc;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int e = tid + 256 * u;
+        if (e < M2) p.Rend[(size_t)c * M2 + e] = R[cur][e];
+    }
+}
+
+// trunk states at the block starts: P[0] = rho_init, P[c + 1] = Rend[c] P[c] (one wave, c < n_chain)
+template <int N2>
+__global__ __launch_bounds__(64) void mcb_chain_kernel(MapChainParams p, int n_chain) {
+    __shared__ double2 x[64];
+    const int lane = threadIdx.x;
+    const bool on = lane < N2;
+    if (on) { x[lane] = p.rho_init[lane]; p.P[lane] = p.rho_init[lane]; }
+    __syncthreads();
+    constexpr int M2 = N2 * N2;
+    double2 am[N2];
+    auto load = [&](int c) {
+        const double2* A = p.Rend + (size_t)c * M2 + (on ? lane : 0);
+#pragma unroll
+        for (int k = 0; k < N2; ++k) am[k] = A[k * N2];
+    };
+    if (n_chain > 0) load(0);
+    for (int c = 0; c < n_chain; ++c) {
+        double2 y = c_zero();
+#pragma unroll
+        for (int k = 0; k < N2; ++k) c_fma(y, am[k], x[k]);
+        if (c + 1 < n_chain) load(c + 1);
+        __syncthreads();
+        if (on) { x[lane] = y; p.P[(size_t)(c + 1) * N2 + lane] = y; }
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ int wave_max_int(int v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// per trajectory: rho(j_i) = E[p_i - 1] ... E[cL] P[c] (c = p_i / L, < L steps), then G(i, 1) = Tr(A B C rho) and
+// the tau start C rho A (propagate_tau.f90:154-163), as mc_trunk_kernel computes them
+template <int N2>
+__global__ __launch_bounds__(64) void mcb_trunk_kernel(MapChainParams p) {
+    constexpr int TPW = 64 / N2;
+    constexpr int M2 = N2 * N2;
+    __shared__ double2 xs[2][64], t1[64], t2[64];
+    const int lane = threadIdx.x, dim = p.dim;
+    const int tl = lane / N2, r = lane - (lane / N2) * N2;
+    const int i = blockIdx.x * TPW + tl;
+    const bool act = (tl < TPW) && (i < p.n_t);
+    const int tlx = tl < TPW ? tl : 0;
+    const int p0 = act ? p.pos[i] : 0;
+    const int c = p0 / p.L;
+    const int ns = act ? p0 - c * p.L : 0;
+    xs[0][lane] = act ? p.P[(size_t)c * N2 + r] : c_zero();
+    const int mx = wave_max_int(ns);
+    double2 am[N2];
+    auto load = [&](int s) {
+        const double2* A = p.dmA + (size_t)(s < ns ? c * p.L + s : 0) * M2 + r;
+#pragma unroll
+        for (int k = 0; k < N2; ++k) am[k] = A[k * N2];
+    };
+    if (mx > 0) load(0);
+    __syncthreads();
+    int cur = 0;
+    for (int s = 0; s < mx; ++s) {
+        const double2* x = xs[cur] + tlx * N2;
+        double2 y = c_zero();
+#pragma unroll
+        for (int k = 0; k < N2; ++k) c_fma(y, am[k], x[k]);
+        if (s + 1 < mx) load(s + 1);
+        xs[cur ^ 1][lane] = (s < ns) ? y : xs[cur][lane];
+        __syncthreads();
+        cur ^= 1;
+    }
+    const double2* X = xs[cur] + tlx * N2;
+    double2* T1 = t1 + tlx * N2;
+    double2* T2 = t2 + tlx * N2;
+    // G(i, 1) = Tr(A (B (C rho)))
+    if (act) T1[r] = cm_mat(p.opC, X, r, dim);
+    __syncthreads();
+    if (act) T2[r] = cm_mat(p.opB, T1, r, dim);
+    __syncthreads();
+    if (act) T1[r] = cm_mat(p.opA, T2, r, dim);
+    __syncthreads();
+    if (act && r == 0) {
+        double2 s = c_zero();
+        for (int l = 0; l < dim; ++l) s = c_add(s, T1[l + l * dim]);
+        p.result[i] = s;
+    }
+    __syncthreads();
+    if (act) T1[r] = cm_mat(p.opC, X, r, dim);
+    __syncthreads();
+    if (act) p.rho_buf[(size_t)i * N2 + r] = cm_mat(T1, p.opA, r, dim);
+}
+
+// per trajectory: the map-by-map steps up to its first block boundary (outputs written) and one Rend matvec per later
+// block (states X_i[c] stored); the loop is pipelined like mc_tau_pipe_kernel
+template <int N2, int PFD>
+__global__ __launch_bounds__(64) void mcb_tau_kernel(MapChainParams p) {
+    constexpr int TPW = 64 / N2;
+    constexpr int M2 = N2 * N2;
+    __shared__ double2 xs[2][64], ts[64];
+    const int lane = threadIdx.x;
+    const int tl = lane / N2, r = lane - (lane / N2) * N2;
+    const int i = blockIdx.x * TPW + tl;
+    const bool act = (tl < TPW) && (i < p.n_t);
+    const int tlx = tl < TPW ? tl : 0;
+    const int L = p.L;
+    const int p0 = act ? p.pos[i] : 0;
+    const int nf = act ? min(p.n_tau, (L - p0 % L) % L) : 0;
+    const bool full = act && nf < p.n_tau;
+    const int cs = (p0 + nf) / L;
+    const int nb = full ? (p0 + p.n_tau - 1) / L - cs : 0;
+    const int ns = nf + nb;
+    const int mx = wave_max_int(ns);
+    const double2 w = act ? trace_weight(p, r) : c_zero();
+    const double2 x0 = act ? p.rho_buf[(size_t)i * N2 + r] : c_zero();
+    xs[0][lane] = x0;
+    if (full && nf == 0) p.X[((size_t)cs * p.n_t + i) * N2 + r] = x0;
+    double2 am[PFD][N2];
+    int sl_next = 0;  // lookahead step index
+    auto load_row = [&](int sl) {
+        const int s = sl_next++;
+        const double2* A = s < nf ? p.dmA + (size_t)(p0 + s) * M2
+                                  : (s < ns ? p.Rend + (size_t)(cs + s - nf) * M2 : p.Rend);
+        A += r;
+#pragma unroll
+        for (int k = 0; k < N2; ++k) am[sl][k] = A[k * N2];
+    };
+#pragma unroll
+    for (int sl = 0; sl < PFD; ++sl) load_row(sl);
+    __syncthreads();
+    int cur = 0;
+    auto step = [&](int sl, int s) {
+        const double2* x = xs[cur] + tlx * N2;
+        double2 y = c_zero();
+#pragma unroll
+        for (int k = 0; k < N2; ++k) c_fma(y, am[sl][k], x[k]);
+        load_row(sl);
+        xs[cur ^ 1][lane] = (s < ns) ? y : xs[cur][lane];
+        ts[lane] = c_mul(w, y);
+        if (s >= nf && s < ns) p.X[((size_t)(cs + s - nf + 1) * p.n_t + i) * N2 + r] = y;
+        else if (full && s == nf - 1) p.X[((size_t)cs * p.n_t + i) * N2 + r] = y;
+        __syncthreads();
+        if (act && r == 0 && s < nf) {
+            double2 g = c_zero();
+#pragma unroll
+            for (int q = 0; q < N2; ++q) g = c_add(g, ts[tl * N2 + q]);
+            p.result[(size_t)i + (size_t)(s + 1) * p.n_t] = g;
+        }
+        cur ^= 1;
+    };
+    int s = 0;
+    for (; s + PFD - 1 < mx; s += PFD) {
+#pragma unroll
+        for (int sl = 0; sl < PFD; ++sl) step(sl, s + sl);
+    }
+#pragma unroll
+    for (int sl = 0; sl < PFD; ++sl)
+        if (s + sl < mx) step(sl, s + sl);
+}
+
+// every output past a trajectory's first block boundary: G(i, s + 2) = U[p_i + s] . X_i[(p_i + s) / L]
+template <int N2>
+__global__ __launch_bounds__(256) void mcb_out_kernel(MapChainParams p) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= p.n_t) return;
+    const int L = p.L;
+    const int p0 = p.pos[i];
+    const int nf = min(p.n_tau, (L - p0 % L) % L);
+    for (int col = blockIdx.y + 1; col <= p.n_tau; col += gridDim.y) {
+        const int s = col - 1;
+        if (s < nf) continue;
+        const int q = p0 + s;
+        const double2* u = p.U + (size_t)q * N2;
+        const double2* x = p.X + ((size_t)(q / L) * p.n_t + i) * N2;
+        double2 g = c_zero();
+#pragma unroll
+        for (int k = 0; k < N2; ++k) c_fma(g, u[k], x[k]);
+        p.result[(size_t)i + (size_t)col * p.n_t] = g;
+    }
+}
+
 __global__ __launch_bounds__(64) void propagate_tau_kernel(const double2* dm, const double2* rho0, int N2,
                                                            int n_tau, int j_start, double2* out) {
     __shared__ double2 x[64];
@@ -423,6 +684,34 @@ hipError_t launch_mapchain(const MapChainParams& p, hipStream_t s) {
     }
     hipLaunchKernelGGL(mc_tau_kernel, dim3(nblk), dim3(64), 0, s, p);
     return hipGetLastError();
+}
+
+template <int N2, int PFD>
+static hipError_t launch_blocked_n(const MapChainParams& p, int n_chain, hipStream_t s) {
+    if (p.n_blk > 0) hipLaunchKernelGGL((mcb_prefix_kernel<N2>), dim3(p.n_blk), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((mcb_chain_kernel<N2>), dim3(1), dim3(64), 0, s, p, n_chain);
+    constexpr int TPW = 64 / N2;
+    const int nblk = (p.n_t + TPW - 1) / TPW;
+    hipLaunchKernelGGL((mcb_trunk_kernel<N2>), dim3(nblk), dim3(64), 0, s, p);
+    if (p.n_tau > 0) {
+        hipLaunchKernelGGL((mcb_tau_kernel<N2, PFD>), dim3(nblk), dim3(64), 0, s, p);
+        const int gy = std::min(p.n_tau, 65535);
+        hipLaunchKernelGGL((mcb_out_kernel<N2>), dim3((p.n_t + 255) / 256, gy), dim3(256), 0, s, p);
+    }
+    return hipGetLastError();
+}
+
+// mode 0 on the blocked sweep; p.pos, p.L, p.n_blk, p.Q and the U / Rend / P / X buffers set by the host;
+// n_chain = max_i p_i / L block starts of the trunk
+hipError_t launch_mapchain_blocked(const MapChainParams& p, int n_chain, hipStream_t s) {
+    switch (p.N2) {
+        case 4: return launch_blocked_n<4, 4>(p, n_chain, s);
+        case 9: return launch_blocked_n<9, 2>(p, n_chain, s);
+        case 16: return launch_blocked_n<16, 2>(p, n_chain, s);
+        case 25: return launch_blocked_n<25, 1>(p, n_chain, s);
+        case 36: return launch_blocked_n<36, 1>(p, n_chain, s);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_propagate_tau(int N2, const double2* dm, const double2* rho0, int n_tau, int j_start,

@@ -150,6 +150,13 @@ struct MapChainParams {
     double2* rho_buf;        // scratch n_t*N2
     int* j_arr;              // scratch n_t
     double2* result;         // (n_t, n_tau+1) column-major
+    // blocked tau sweep (mode 0, mapchain.hip "blocked"): positions q = map index 0.., blocks of L positions
+    int L, n_blk, Q;         // block length, blocks, positions with maps [0, Q)
+    const int* pos;          // n_t: p_i = j_i - 1, host-computed trunk end (first tau map)
+    double2* U;              // Q*N2: U[q] = w^T E[q] ... E[cL] (c = q / L)
+    double2* Rend;           // n_blk*N2*N2: E[end of block c] ... E[cL], column-major
+    double2* P;              // n_blk*N2: trunk state before block c
+    double2* X;              // n_blk*n_t*N2: trajectory i's tau state before block c
 };
 
 struct FourTimeParams {
@@ -204,6 +211,7 @@ hipError_t launch_sweep(int N2, int CHI, int BT, int n_blocks, const SweepParams
 int sweep_max_bt(int N2);
 hipError_t launch_sweep_nopt(int N2, int n_blocks, const SweepParams& p, hipStream_t s);
 hipError_t launch_mapchain(const MapChainParams& p, hipStream_t s);
+hipError_t launch_mapchain_blocked(const MapChainParams& p, int n_chain, hipStream_t s);
 hipError_t launch_four_time(const FourTimeParams& p, hipStream_t s);
 hipError_t launch_propagate_tau(int N2, const double2* dm, const double2* rho0, int n_tau, int j_start,
                                 double2* out, hipStream_t s);

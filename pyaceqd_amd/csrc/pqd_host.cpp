@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <climits>
 #include <memory>
+#include <cmath>
 #include <complex>
 #include <cstdarg>
 #include <cstdio>
@@ -1243,7 +1244,41 @@ static int mapchain_run(pqd_ctx* ctx, MapChainParams& p, const pqd_c128* dmA, si
     p.dmA = A.p; p.dmB = Bm.p; p.dmT = Tm.p; p.dm_s = Ds.p; p.rho_init = r0.p;
     p.opA = oa.p; p.opB = ob.p; p.opC = oc.p; p.time = tm.p; p.time_sparse = ts.p;
     p.rho_buf = rb.p; p.j_arr = ja.p; p.result = res.p;
-    HIPCHK(launch_mapchain(p, s));
+    // calc_onetime_parallel on the blocked sweep (mapchain.hip): the trunk ends j_i are found here with the
+    // Fortran's own comparisons (propagate_tau.f90:144-151), which also bounds every map the sweep reads
+    DevBuf<double2> U, Rend, Pb, Xb;
+    DevBuf<int> posd;
+    const char* eb = getenv("PQD_MC_BLOCKED");
+    const bool blocked = p.mode == 0 && !(eb && atoi(eb) == 0) &&
+                         (N2 == 4 || N2 == 9 || N2 == 16 || N2 == 25 || N2 == 36);
+    if (blocked) {
+        std::vector<int> pos(p.n_t);
+        int j = 1, pmax = 0, Q = 0;
+        for (int i = 0; i < p.n_t; ++i) {
+            while (j <= p.n_tfull && time[j - 1] < time_sparse[i]) ++j;
+            pos[i] = j - 1;
+            pmax = std::max(pmax, j - 1);
+            Q = std::max(Q, j - 1 + p.n_tau);
+        }
+        if ((size_t)std::max(Q, pmax) > nA)
+            return fail(PQD_ERR_ARG, "the sweep would read map %d of %zu (time_sparse beyond time, or n_tau too long "
+                        "for dm_tl)", std::max(Q, pmax), nA);
+        const char* el = getenv("PQD_MC_L");
+        int L = el ? atoi(el) : (int)std::lround(std::sqrt((double)std::max(1, p.n_tau)));
+        L = std::max(8, std::min(256, L));
+        p.L = L;
+        p.Q = std::max(Q, 1);
+        p.n_blk = (p.Q + L - 1) / L;
+        HIPCHK(posd.upload(pos.data(), p.n_t, s));
+        HIPCHK(U.alloc((size_t)p.Q * N2));
+        HIPCHK(Rend.alloc((size_t)p.n_blk * m2));
+        HIPCHK(Pb.alloc((size_t)(p.n_blk + 1) * N2));
+        HIPCHK(Xb.alloc((size_t)p.n_blk * p.n_t * N2));
+        p.pos = posd.p; p.U = U.p; p.Rend = Rend.p; p.P = Pb.p; p.X = Xb.p;
+        HIPCHK(launch_mapchain_blocked(p, pmax / L, s));
+    } else {
+        HIPCHK(launch_mapchain(p, s));
+    }
     HIPCHK(hipMemcpyAsync(result, res.p, nres * sizeof(double2), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     return PQD_OK;

@@ -262,8 +262,9 @@ def _c5_worker(rank, world, port, q):
 @pytest.mark.gpu
 def test_gloo_world2_c5_scan_sharded_matches_single_process(tmp_path):
     """BASELINE config 5's tomography scan sharded over two ranks (a contiguous block of grid points
-    per rank, two processes on the one GPU), (concurrence, rho) gathered to rank 0: bit-identical to the scan in one
-    process"""
+    per rank, two processes on the one GPU), (concurrence, rho) gathered to rank 0: equal to the scan in one process
+    to rounding (a two-point launch may take other, parity-tested, kernel paths than the four-point one: the trunk
+    pre-pass and split-group choices depend on the batch)"""
     from tests.test_gpu_c5 import BXS, E0S, _point, _pt
     from pyaceqd_amd.pol_entanglement.G2 import densitymatrix_reuse_scan
     from pyaceqd_amd.six_level_system.linear import sixls_linear
@@ -273,5 +274,5 @@ def test_gloo_world2_c5_scan_sharded_matches_single_process(tmp_path):
     ref = densitymatrix_reuse_scan(insts, [{"bx": bx} for e0 in E0S for bx in BXS], return_rho=True)
     assert len(got) == len(ref) == 4
     for (cg, rg), (cr, rr) in zip(got, ref):
-        assert cg == cr
-        assert np.array_equal(rg, rr)
+        assert abs(cg - cr) < 1e-12
+        assert np.max(np.abs(rg - rr)) <= 1e-12 * np.max(np.abs(rr))

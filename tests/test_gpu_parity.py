@@ -320,6 +320,44 @@ def test_mapchain_large_vs_oracle():
     assert rel(a, b) < 1e-11
 
 
+@pytest.mark.parametrize("dim", [2, 3, 4, 5, 6])
+@pytest.mark.parametrize("L", ["8", "13", "0"])
+def test_mapchain_blocked_sweep_vs_oracle(monkeypatch, dim, L):
+    """calc_onetime_parallel on the blocked sweep (per-block prefix products, mapchain.hip mcb_*) for block lengths
+    8 / 13 / auto (sqrt(n_tau)), trajectories that start on, just before and just after block boundaries, repeated
+    and off-grid t1 points, a t1 point past the grid, vs the C oracle and vs the map-by-map pipelined kernel"""
+    from pyaceqd_amd.two_time import propagate_tau_module as M
+    if L != "0":
+        monkeypatch.setenv("PQD_MC_L", L)
+    rng = np.random.default_rng(dim)
+    N2 = dim * dim
+    n_tau, n_tfull = 150, 260
+    maps = np.stack([np.eye(N2) + 0.05 * (rng.normal(size=(N2, N2)) + 1j * rng.normal(size=(N2, N2))) / dim
+                     for _ in range(n_tfull - 1)])
+    time = np.round(np.arange(n_tfull) * 0.1, 6)
+    ts = np.array([0.0, 0.05, 0.7, 0.75, 0.8, 0.8, 1.2, 1.3, 1.31, 2.55, 4.0, 6.4, 7.9, 10.0, 10.85])
+    ops = [rng.normal(size=(dim, dim)) + 1j * rng.normal(size=(dim, dim)) for _ in range(3)]
+    rho = H.random_rho(dim).reshape(N2)
+    a = M.calc_onetime_parallel(F(maps), rho, n_tau, dim, *ops, time, ts)
+    b = oracle.calc_onetime_parallel(F(maps), rho, n_tau, dim, *ops, time, ts, nthreads=8)
+    assert rel(a, b) < 1e-11
+    monkeypatch.setenv("PQD_MC_BLOCKED", "0")
+    c = M.calc_onetime_parallel(F(maps), rho, n_tau, dim, *ops, time, ts)
+    assert rel(a, c) < 1e-11
+
+
+def test_mapchain_blocked_refuses_reads_past_the_maps():
+    """a tau window running past the last map is refused (the Fortran would read past dm_tl)"""
+    from pyaceqd_amd.two_time import propagate_tau_module as M
+    dim, N2, n_tfull = 2, 4, 30
+    maps = np.stack([np.eye(N2, dtype=complex)] * (n_tfull - 1))
+    time = np.round(np.arange(n_tfull) * 0.1, 6)
+    ops = [np.eye(dim, dtype=complex)] * 3
+    with pytest.raises(ValueError, match="would read map"):
+        M.calc_onetime_parallel(F(maps), np.eye(dim, dtype=complex).reshape(N2), 25, dim, *ops, time,
+                                np.array([0.0, 0.5]))
+
+
 # --------------------------------------------------------------------------------- time-local maps
 def test_tl_dynmap_vs_reference_golden(golden_dir):
     """GPU Jacobi-SVD pinv time-localisation vs the reference's calc_tl_dynmap_pseudo (tools.py:446-484)
