@@ -238,6 +238,15 @@ __global__ __launch_bounds__(64) void mc_tau_pipe_kernel(MapChainParams p) {
 // (mcb_out_kernel, all (i, tau) in parallel). Same products as the reference's chain, associated per block:
 // results agree to rounding (the Fortran goldens and the pipelined kernel, PQD_MC_BLOCKED=0).
 // ---------------------------------------------------------------------------------------------
+// the map at position q of the shared sequence: mode 0 dm_tl(:, :, q + 1); mode 1 (calc_onetime_parallel_block) the
+// periodic sequence jj = q mod n_tb + 1 -> dm_block(:, :, jj) for jj <= n_map, else dm_s (propagate_tau.f90:270-287)
+__device__ __forceinline__ const double2* map_at(const MapChainParams& p, int q, int M2) {
+    if (p.mode == 0) return p.dmA + (size_t)q * M2;
+    if (q >= p.q_s) return p.dm_s;
+    const int jj = q % p.n_tb + 1;
+    return jj <= p.n_map ? p.dmA + (size_t)(jj - 1) * M2 : p.dm_s;
+}
+
 __device__ __forceinline__ double2 trace_weight(const MapChainParams& p, int r) {
     // Tr(opB R) over the column-major view of R (propagate_tau.f90:176): lane r = b + a dim gets opB(a, b)
     const int a = r / p.dim, b = r % p.dim;
@@ -256,7 +265,7 @@ __global__ __launch_bounds__(256) void mcb_prefix_kernel(MapChainParams p) {
     if (tid < N2) w[tid] = trace_weight(p, tid);
     double2 nx[PER];
     auto fetch = [&](int q) {
-        const double2* A = p.dmA + (size_t)q * M2;
+        const double2* A = map_at(p, q, M2);
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const int e = tid + 256 * u;
@@ -427,7 +436,7 @@ __global__ __launch_bounds__(64) void mcb_tau_kernel(MapChainParams p) {
     int sl_next = 0;  // lookahead step index
     auto load_row = [&](int sl) {
         const int s = sl_next++;
-        const double2* A = s < nf ? p.dmA + (size_t)(p0 + s) * M2
+        const double2* A = s < nf ? map_at(p, p0 + s, M2)
                                   : (s < ns ? p.Rend + (size_t)(cs + s - nf) * M2 : p.Rend);
         A += r;
 #pragma unroll
@@ -689,10 +698,16 @@ hipError_t launch_mapchain(const MapChainParams& p, hipStream_t s) {
 template <int N2, int PFD>
 static hipError_t launch_blocked_n(const MapChainParams& p, int n_chain, hipStream_t s) {
     if (p.n_blk > 0) hipLaunchKernelGGL((mcb_prefix_kernel<N2>), dim3(p.n_blk), dim3(256), 0, s, p);
-    hipLaunchKernelGGL((mcb_chain_kernel<N2>), dim3(1), dim3(64), 0, s, p, n_chain);
     constexpr int TPW = 64 / N2;
     const int nblk = (p.n_t + TPW - 1) / TPW;
-    hipLaunchKernelGGL((mcb_trunk_kernel<N2>), dim3(nblk), dim3(64), 0, s, p);
+    if (p.mode == 0) {
+        hipLaunchKernelGGL((mcb_chain_kernel<N2>), dim3(1), dim3(64), 0, s, p, n_chain);
+        hipLaunchKernelGGL((mcb_trunk_kernel<N2>), dim3(nblk), dim3(64), 0, s, p);
+    } else {
+        // mode 1: the trunk runs dm_block then dm_s without wrapping (propagate_tau.f90:235-241), a different
+        // sequence from the periodic tau maps: the serial trunk kernel
+        hipLaunchKernelGGL(mc_trunk_kernel, dim3(1), dim3(64), 0, s, p);
+    }
     if (p.n_tau > 0) {
         hipLaunchKernelGGL((mcb_tau_kernel<N2, PFD>), dim3(nblk), dim3(64), 0, s, p);
         const int gy = std::min(p.n_tau, 65535);
@@ -701,8 +716,8 @@ static hipError_t launch_blocked_n(const MapChainParams& p, int n_chain, hipStre
     return hipGetLastError();
 }
 
-// mode 0 on the blocked sweep; p.pos, p.L, p.n_blk, p.Q and the U / Rend / P / X buffers set by the host;
-// n_chain = max_i p_i / L block starts of the trunk
+// modes 0 and 1 on the blocked sweep; p.pos, p.L, p.n_blk, p.Q and the U / Rend / P / X buffers set by the host;
+// n_chain = max_i p_i / L block starts of the trunk (mode 0)
 hipError_t launch_mapchain_blocked(const MapChainParams& p, int n_chain, hipStream_t s) {
     switch (p.N2) {
         case 4: return launch_blocked_n<4, 4>(p, n_chain, s);

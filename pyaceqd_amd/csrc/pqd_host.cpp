@@ -7,6 +7,7 @@
 #include "pqd_common.h"
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
 #include <memory>
 #include <cmath>
@@ -16,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -178,7 +180,47 @@ void build_generators(const pqd_system* sys, Generators& G) {
 struct pqd_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // map-chain sweeps: one device arena reused across calls (grown on demand), so a call allocates nothing
+    DevBuf<char> mc_arena;
 };
+
+namespace {
+int Q_of(const std::vector<int>& pos, int n_tau) {
+    int q = 0;
+    for (int v : pos) q = std::max(q, v + n_tau);
+    return q;
+}
+
+// write one byte per 4 KiB page of a host output buffer (its contents are overwritten afterwards), on up to 8
+// threads for buffers of several MB
+void touch_pages(void* buf, size_t bytes) {
+    if (bytes < ((size_t)1 << 20)) return;
+    char* b = static_cast<char*>(buf);
+    const int nth = (int)std::min<size_t>(8, bytes >> 22) + 1;
+    const size_t chunk = ((bytes / nth) + 4095) & ~(size_t)4095;
+    auto work = [=](int k) {
+        volatile char* q = b;
+        for (size_t o = (size_t)k * chunk; o < std::min(bytes, (size_t)(k + 1) * chunk); o += 4096) q[o] = 0;
+    };
+    std::vector<std::thread> th;
+    for (int k = 1; k < nth; ++k) th.emplace_back(work, k);
+    work(0);
+    for (auto& t : th) t.join();
+}
+
+// consecutive 256-B aligned sub-buffers of one device allocation (size pass with base == nullptr)
+struct Carve {
+    char* base = nullptr;
+    size_t off = 0;
+    template <class T>
+    T* take(size_t count) {
+        off = (off + 255) & ~(size_t)255;
+        T* r = base ? reinterpret_cast<T*>(base + off) : nullptr;
+        off += count * sizeof(T);
+        return r;
+    }
+};
+}  // namespace
 
 struct pqd_pt {
     pqd_ctx* ctx = nullptr;
@@ -955,10 +997,13 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     HIPCHK(P->flags.alloc(4));
     HIPCHK(hipMemsetAsync(P->flags.p, 0, 4 * sizeof(unsigned), s));
     sp.flags = P->flags.p;
-    { const char* pm = getenv("PQD_PT_MODE"); sp.pt_mode = pm ? atoi(pm) : 4; }
+    // PT rows: 3M on the matrix cores; at BT = 4 (N2 > 16, chi = 128) with two k-steps of the slice in flight
+    // (six-level scan c5: 84.7 -> 79.5 ms per launch, profiles/r03/exp_c/c5_ptmode.log)
+    { const char* pm = getenv("PQD_PT_MODE"); sp.pt_mode = pm ? atoi(pm) : (P->BT == 4 ? 5 : 4); }
     { const char* c3 = getenv("PQD_CMUL3"); sp.cmul3 = c3 ? atoi(c3) : 1; }
+    { const char* c4 = getenv("PQD_COL44"); sp.col44 = c4 ? atoi(c4) : 1; }
     { const char* tp = getenv("PQD_TRPRE"); sp.trpre = tp ? atoi(tp) : 1; }
-    if (pt && (sp.pt_mode == 4 || sp.pt_mode == 5)) {
+    if (pt && (sp.pt_mode == 4 || sp.pt_mode == 5 || sp.pt_mode == 6)) {
         const int nw = P->BT * sweep_wpt(P->N2, P->BT, P->CHI);
         int rmax = sweep_rmax(P->N2, P->BT, P->CHI);
         if (const char* e = getenv("PQD_ROWPAIR")) rmax = std::max(1, std::min(rmax, atoi(e) ? rmax : 1));
@@ -967,6 +1012,11 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
         sp.units = P->units.p;
         sp.umax = (int)(u.size() / nw);
     }
+    // the production sweep instance holds the default variants only (3M rows from the unit list with one or two
+    // k-steps in flight, 3M columns on 4x4x4 tiles where N2 is not a multiple of 16); anything else runs the A/B
+    // instance (pt_sweep_all.hip)
+    sp.variants = !(sp.units && (sp.pt_mode == 4 || sp.pt_mode == 5) && sp.cmul3 == 1 &&
+                    (sp.col44 == 1 || N2 % 16 == 0)) ? 1 : 0;
     { const char* fz = getenv("PQD_FUSE"); sp.fuse = (!P->nopt && ns > 0 && (fz ? atoi(fz) : 1)) ? 1 : 0; }
     if (!sp.fuse) sp.trpre = 0;  // the prefetched rows are W(n), which exists only with fused half steps
     if (sp.fuse) {
@@ -1220,67 +1270,122 @@ static int mapchain_run(pqd_ctx* ctx, MapChainParams& p, const pqd_c128* dmA, si
     const int N2 = p.dim * p.dim;
     p.N2 = N2;
     const size_t m2 = (size_t)N2 * N2;
-    DevBuf<double2> A, Bm, Tm, Ds, r0, oa, ob, oc, rb, res;
-    DevBuf<double> tm, ts;
-    DevBuf<int> ja;
-    auto up = [&](DevBuf<double2>& b, const pqd_c128* src, size_t n) {
-        return b.upload(reinterpret_cast<const double2*>(src), n, s);
-    };
-    HIPCHK(up(A, dmA, nA * m2));
-    if (dmB) HIPCHK(up(Bm, dmB, nB * m2));
-    if (dmT) HIPCHK(up(Tm, dmT, nT * m2));
-    if (dm_s) HIPCHK(up(Ds, dm_s, m2));
-    HIPCHK(up(r0, rho_init, N2));
-    HIPCHK(up(oa, opA, N2));
-    HIPCHK(up(ob, opB, N2));
-    HIPCHK(up(oc, opC, N2));
-    HIPCHK(tm.upload(time, p.n_tfull, s));
-    HIPCHK(ts.upload(time_sparse, p.n_t, s));
-    HIPCHK(rb.alloc((size_t)p.n_t * N2));
-    HIPCHK(ja.alloc(p.n_t));
     const size_t nres = (size_t)p.n_t * (p.n_tau + 1);
-    HIPCHK(res.alloc(nres));
-    HIPCHK(hipMemsetAsync(res.p, 0, nres * sizeof(double2), s));
-    p.dmA = A.p; p.dmB = Bm.p; p.dmT = Tm.p; p.dm_s = Ds.p; p.rho_init = r0.p;
-    p.opA = oa.p; p.opB = ob.p; p.opC = oc.p; p.time = tm.p; p.time_sparse = ts.p;
-    p.rho_buf = rb.p; p.j_arr = ja.p; p.result = res.p;
     // calc_onetime_parallel on the blocked sweep (mapchain.hip): the trunk ends j_i are found here with the
     // Fortran's own comparisons (propagate_tau.f90:144-151), which also bounds every map the sweep reads
-    DevBuf<double2> U, Rend, Pb, Xb;
-    DevBuf<int> posd;
     const char* eb = getenv("PQD_MC_BLOCKED");
-    const bool blocked = p.mode == 0 && !(eb && atoi(eb) == 0) &&
-                         (N2 == 4 || N2 == 9 || N2 == 16 || N2 == 25 || N2 == 36);
+    bool blocked = (p.mode == 0 || p.mode == 1) && !(eb && atoi(eb) == 0) &&
+                   (N2 == 4 || N2 == 9 || N2 == 16 || N2 == 25 || N2 == 36);
+    std::vector<int> pos;
+    int pmax = 0;
     if (blocked) {
-        std::vector<int> pos(p.n_t);
-        int j = 1, pmax = 0, Q = 0;
+        pos.resize(p.n_t);
+        int j = 1;
         for (int i = 0; i < p.n_t; ++i) {
             while (j <= p.n_tfull && time[j - 1] < time_sparse[i]) ++j;
             pos[i] = j - 1;
             pmax = std::max(pmax, j - 1);
-            Q = std::max(Q, j - 1 + p.n_tau);
         }
-        if ((size_t)std::max(Q, pmax) > nA)
+        if (p.mode == 1) {
+            // a trunk that ends past the first period (j > n_tb) never wraps in the tau loop (:270-287: jj resets
+            // only when it equals n_tb + 1), so that trajectory applies dm_s at every tau step: it starts at q_s, the
+            // first position of a constant dm_s region placed after the periodic positions (map_at)
+            int qp = 0;
+            bool any_s = false;
+            for (int i = 0; i < p.n_t; ++i) {
+                if (pos[i] + 1 <= p.n_tb) qp = std::max(qp, pos[i] + p.n_tau);
+                else any_s = true;
+            }
+            p.q_s = any_s ? qp : INT_MAX;
+            for (int i = 0; i < p.n_t; ++i)
+                if (pos[i] + 1 > p.n_tb) pos[i] = p.q_s;
+        }
+    }
+    if (blocked) {
+        if (p.mode == 0 && (size_t)std::max(Q_of(pos, p.n_tau), pmax) > nA)
             return fail(PQD_ERR_ARG, "the sweep would read map %d of %zu (time_sparse beyond time, or n_tau too long "
-                        "for dm_tl)", std::max(Q, pmax), nA);
+                        "for dm_tl)", std::max(Q_of(pos, p.n_tau), pmax), nA);
+        const int Q = Q_of(pos, p.n_tau);
         const char* el = getenv("PQD_MC_L");
         int L = el ? atoi(el) : (int)std::lround(std::sqrt((double)std::max(1, p.n_tau)));
         L = std::max(8, std::min(256, L));
         p.L = L;
         p.Q = std::max(Q, 1);
         p.n_blk = (p.Q + L - 1) / L;
-        HIPCHK(posd.upload(pos.data(), p.n_t, s));
-        HIPCHK(U.alloc((size_t)p.Q * N2));
-        HIPCHK(Rend.alloc((size_t)p.n_blk * m2));
-        HIPCHK(Pb.alloc((size_t)(p.n_blk + 1) * N2));
-        HIPCHK(Xb.alloc((size_t)p.n_blk * p.n_t * N2));
-        p.pos = posd.p; p.U = U.p; p.Rend = Rend.p; p.P = Pb.p; p.X = Xb.p;
-        HIPCHK(launch_mapchain_blocked(p, pmax / L, s));
+    }
+    // every device buffer of the call carved from the context's arena
+    auto carve = [&](Carve& c) {
+        p.dmA = c.take<double2>(nA * m2);
+        p.dmB = dmB ? c.take<double2>(nB * m2) : nullptr;
+        p.dmT = dmT ? c.take<double2>(nT * m2) : nullptr;
+        p.dm_s = dm_s ? c.take<double2>(m2) : nullptr;
+        p.rho_init = c.take<double2>(N2);
+        p.opA = c.take<double2>(N2);
+        p.opB = c.take<double2>(N2);
+        p.opC = c.take<double2>(N2);
+        p.time = c.take<double>(p.n_tfull);
+        p.time_sparse = c.take<double>(p.n_t);
+        p.rho_buf = c.take<double2>((size_t)p.n_t * N2);
+        p.j_arr = c.take<int>(p.n_t);
+        p.result = c.take<double2>(nres);
+        if (blocked) {
+            p.pos = c.take<int>(p.n_t);
+            p.U = c.take<double2>((size_t)p.Q * N2);
+            p.Rend = c.take<double2>((size_t)p.n_blk * m2);
+            p.P = c.take<double2>((size_t)(p.n_blk + 1) * N2);
+            p.X = c.take<double2>((size_t)p.n_blk * p.n_t * N2);
+        }
+    };
+    Carve sz;
+    carve(sz);
+    if (ctx->mc_arena.n < sz.off + 256) {
+        HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(ctx->mc_arena.alloc(sz.off + sz.off / 4 + 256));
+    }
+    Carve cv;
+    cv.base = ctx->mc_arena.p;
+    carve(cv);
+    auto up = [&](const void* dst, const void* src, size_t bytes) {
+        return bytes ? hipMemcpyAsync(const_cast<void*>(dst), src, bytes, hipMemcpyHostToDevice, s) : hipSuccess;
+    };
+    // PQD_MC_TIMING=1: host-side phase times of this call on stderr (diagnostics)
+    const bool tmg = getenv("PQD_MC_TIMING") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    const auto t0 = now();
+    HIPCHK(up(p.dmA, dmA, nA * m2 * sizeof(double2)));
+    if (dmB) HIPCHK(up(p.dmB, dmB, nB * m2 * sizeof(double2)));
+    if (dmT) HIPCHK(up(p.dmT, dmT, nT * m2 * sizeof(double2)));
+    if (dm_s) HIPCHK(up(p.dm_s, dm_s, m2 * sizeof(double2)));
+    HIPCHK(up(p.rho_init, rho_init, N2 * sizeof(double2)));
+    HIPCHK(up(p.opA, opA, N2 * sizeof(double2)));
+    HIPCHK(up(p.opB, opB, N2 * sizeof(double2)));
+    HIPCHK(up(p.opC, opC, N2 * sizeof(double2)));
+    HIPCHK(up(p.time, time, p.n_tfull * sizeof(double)));
+    HIPCHK(up(p.time_sparse, time_sparse, p.n_t * sizeof(double)));
+    if (blocked) {
+        // every result element is written by the blocked kernels (trunk column, partial-block outputs, dots)
+        HIPCHK(up(p.pos, pos.data(), p.n_t * sizeof(int)));
+        HIPCHK(launch_mapchain_blocked(p, pmax / p.L, s));
     } else {
+        HIPCHK(hipMemsetAsync(p.result, 0, nres * sizeof(double2), s));
         HIPCHK(launch_mapchain(p, s));
     }
-    HIPCHK(hipMemcpyAsync(result, res.p, nres * sizeof(double2), hipMemcpyDeviceToHost, s));
+    // the caller's result array is typically fresh (f2py-style: np.zeros, pages not yet mapped): fault its pages in
+    // on a few host threads while the kernels run, so the copy back runs at the link rate (a 41 MB copy into fresh
+    // pages: 2.4 ms, into mapped ones 0.76 ms; scripts/ubench_h2d.py)
+    const auto t1 = now();
+    touch_pages(result, nres * sizeof(double2));
+    const auto t2 = now();
+    if (tmg) HIPCHK(hipStreamSynchronize(s));
+    const auto t3 = now();
+    HIPCHK(hipMemcpyAsync(result, p.result, nres * sizeof(double2), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    if (tmg) {
+        const auto t4 = now();
+        auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        fprintf(stderr, "pqd mapchain: upload+launch %.3f ms, page touch %.3f ms, kernels left %.3f ms, download %.3f ms\n",
+                ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, t4));
+    }
     return PQD_OK;
 }
 

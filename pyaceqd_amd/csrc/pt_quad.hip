@@ -415,8 +415,10 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : 1) voi
         return n != next_act && n < q_hi && n < n_hi && fuse && NO <= 4 && !(p.ablate & 31) &&
                !__ballot(traj >= 0 && (n < act || !fz || evn.x == n || evn.x == n + 1));
     };
-    auto fast = [&](const int n) {
-        constexpr int S = 0;
+    // ring slot S (compile time): step n's operands; after use the slot fetches step n + 2 (no register moves,
+    // so each fetch has two steps to arrive; see the loop below)
+    auto fast = [&](const int n, auto slot) {
+        constexpr int S = decltype(slot)::value;
         auto stamp = [&](int k) {
             if constexpr (STAMP) {
                 if (blockIdx.x == 0 && threadIdx.x == 0 && n >= 1000 && n < 1016)
@@ -467,8 +469,10 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : 1) voi
                 p.out[wo2 + (long long)(n - wb2) * NO + k2] = x;
         }
         // ring loads of step n + 2 into the slot this step used
-        const int s1 = __builtin_amdgcn_readfirstlane(sr[0]);  // sched[n + 1]
-        shift_ring(n);
+        const int s1 = __builtin_amdgcn_readfirstlane(sr[S]);  // sched[n + 1]
+        fpre[S] = ldF(n + 2);
+        ldW(S, n + 2);
+        sr[S] = ldS(n + 3);
         stamp(3);
         double2 D[NCG];
 #pragma unroll
@@ -487,16 +491,25 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : 1) voi
             for (int cg = 0; cg < NCG; ++cg) R[cg] = sn[crow + 4 * cg];
         }
         stamp(5);
-        // a new slice (or closure) for step n + 1 only when the schedule changes
-        if (q_cur != c_cur) { load_closure(q_cur); c_cur = q_cur; }
-        if (s1 != q_cur) { load_slices(s1); q_cur = s1; }
+        // a new slice (or closure) for step n + 1 only when the schedule changes. The wait sits inside the branch: a
+        // load that MAY be in flight at the join makes the compiler wait for every older load at the first use
+        // (vmcnt counts in order), i.e. for the ring fetches of step n + 2 just issued, on every step
+        if (q_cur != c_cur || s1 != q_cur) {
+            if (q_cur != c_cur) { load_closure(q_cur); c_cur = q_cur; }
+            if (s1 != q_cur) { load_slices(s1); q_cur = s1; }
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        }
         stamp(6);
     };
     for (int n = n0;; ++n) {
-        // runs of fast steps in a loop of their own (one loop body: the compiler's wait counts stay exact)
-        while (fast_ok(n)) {
-            fast(n);
-            ++n;
+        // runs of fast step PAIRS in a loop of their own, one straight-line body over the two ring slots (slot 0
+        // holds step n, slot 1 step n + 1 at the top of every pair; each slot fetches two steps ahead, no register
+        // moves, so the compiler's wait counts never drain a fetch early). A fast step leaves the state fast_ok
+        // reads unchanged, so both steps of a pair are checked up front; an odd step left over takes step()
+        while (fast_ok(n) && fast_ok(n + 1)) {
+            fast(n, std::integral_constant<int, 0>{});
+            fast(n + 1, std::integral_constant<int, 1>{});
+            n += 2;
         }
         if (step(n)) break;
     }

@@ -36,14 +36,17 @@ def _ops(dim, seed):
 
 
 def _time(fn, reps):
-    fn()
-    t0 = time.perf_counter()
+    """median wall time of `reps` calls after one warm-up call (the same statistic for the GPU and the CPU side)"""
+    out = fn()
+    ts = []
     for _ in range(reps):
+        t0 = time.perf_counter()
         out = fn()
-    return (time.perf_counter() - t0) / reps, out
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), out
 
 
-def case_onetime(dim, n_t=256, n_tau=10000, reps=3, cpu=True):
+def case_onetime(dim, n_t=256, n_tau=10000, reps=5, cpu=True):
     from pyaceqd_amd.two_time import propagate_tau_module as gpu
     dt = 0.1
     n_tfull = n_t + n_tau + 2
@@ -60,14 +63,14 @@ def case_onetime(dim, n_t=256, n_tau=10000, reps=3, cpu=True):
     if cpu:
         from oracle import fref
         if fref.available():
-            elc, ref = _time(lambda: fref.calc_onetime_parallel(*args), 1)
+            elc, ref = _time(lambda: fref.calc_onetime_parallel(*args), 3)
             row.update(cpu_ref_wall_s=elc, cpu_ref_traj_steps_per_s=n_t * n_tau / elc,
                        max_rel_diff=float(np.max(np.abs(got - ref)) / np.max(np.abs(ref))),
                        speedup=elc / el)
     return row
 
 
-def case_block(dim=4, n_t=256, n_tb=100, nx_tau=100, reps=3, cpu=True):
+def case_block(dim=4, n_t=256, n_tb=100, nx_tau=100, reps=5, cpu=True):
     from pyaceqd_amd.two_time import propagate_tau_module as gpu
     dt = 0.1
     dm_block = _maps(n_tb, dim, seed=11)
@@ -86,7 +89,7 @@ def case_block(dim=4, n_t=256, n_tb=100, nx_tau=100, reps=3, cpu=True):
     if cpu:
         from oracle import fref
         if fref.available():
-            elc, ref = _time(lambda: fref.calc_onetime_parallel_block(*args), 1)
+            elc, ref = _time(lambda: fref.calc_onetime_parallel_block(*args), 3)
             row.update(cpu_ref_wall_s=elc, cpu_ref_traj_steps_per_s=steps / elc,
                        max_rel_diff=float(np.max(np.abs(got - ref)) / np.max(np.abs(ref))), speedup=elc / el)
     return row
@@ -111,7 +114,7 @@ def case_ft8(dim=4, n_t=128, reps=3, cpu=True):
         from oracle import fref
         if fref.available():
             elc, ref = _time(lambda: fref.four_time_8op(dm1, dm2, rho0, t1, precalc, dt, dim, ops8, False, False,
-                                                        tb), 1)
+                                                        tb), 3)
             row.update(cpu_ref_wall_s=elc, max_rel_diff=float(np.max(np.abs(got - ref)) / np.max(np.abs(ref))),
                        speedup=elc / el)
     return row

@@ -73,6 +73,15 @@ def main():
         for _ in range(args.reps):
             t0 = time.perf_counter(); np.copyto(pin_np, host); ts.append(time.perf_counter() - t0)
         row["host_memcpy_into_pinned_ms"] = 1e3 * min(ts)
+        # what an f2py-style call pays: the result array is new (np.zeros: untouched pages, faulted in by the copy)
+        ts = []
+        for _ in range(args.reps):
+            t0 = time.perf_counter()
+            fresh = np.zeros(n // 8, dtype=np.float64)
+            ok(hip.hipMemcpy(fresh.ctypes.data_as(C.c_void_p), dev, n, 2))
+            ts.append(time.perf_counter() - t0)
+            del fresh
+        row["d2h_fresh_zeros_ms"] = 1e3 * min(ts)
         for k in list(row):
             if k.endswith("_ms") and k != "register_only_ms":
                 row[k.replace("_ms", "_GBs")] = n / (row[k] * 1e-3) / 1e9

@@ -222,13 +222,13 @@ def _c5_per_point(insts, kws):
 
 
 def test_config5_tomography_scan_chi64_vs_per_point_runs(tmp_path):
-    """chi = 64 dictionary PT, the class's own (non-regular) t1 grid, tend 120 ps (past the chirped pulses' end, as
-    construct_t requires): 2 e0 x 2 bx points"""
+    """chi = 64 dictionary PT, the class's own (non-regular) t1 grid, tend 180 ps, the chirped pulses (4 tau = 60 ps) inside
+    [0, tend] as construct_t requires: 2 e0 x 2 bx points"""
     from pyaceqd_amd.pol_entanglement.G2 import densitymatrix_reuse_scan
-    insts, kws = _c5_insts(120.0, tmp_path, t0=10.0, t0b=30.0)
+    insts, kws = _c5_insts(180.0, tmp_path, t0=62.0, t0b=92.0)
     got = densitymatrix_reuse_scan(insts, kws, return_rho=True)
-    assert len(insts[0].t1) > 100 and max(insts[0].t1) <= 120.0
-    ref = _c5_per_point(*_c5_insts(120.0, tmp_path, t0=10.0, t0b=30.0))
+    assert len(insts[0].t1) > 100 and 0 <= min(insts[0].t1) and max(insts[0].t1) <= 180.0
+    ref = _c5_per_point(*_c5_insts(180.0, tmp_path, t0=62.0, t0b=92.0))
     for (cg, rg), (cr, rr) in zip(got, ref):
         assert rg.shape == (4, 4)
         assert np.max(np.abs(rg - rr)) <= 1e-11 * np.max(np.abs(rr))

@@ -346,6 +346,34 @@ def test_mapchain_blocked_sweep_vs_oracle(monkeypatch, dim, L):
     assert rel(a, c) < 1e-11
 
 
+@pytest.mark.parametrize("dim", [2, 4, 6])
+@pytest.mark.parametrize("L", ["8", "0"])
+def test_mapchain_blocked_sweep_block_mode_vs_oracle(monkeypatch, dim, L):
+    """calc_onetime_parallel_block on the blocked sweep: the periodic map sequence (dm_block for the first n_map of
+    every n_tb, then dm_s), trunks ending inside and past the first period (those apply dm_s at every tau step,
+    propagate_tau.f90:270-287), vs the C oracle and the map-by-map kernel"""
+    from pyaceqd_amd.two_time import propagate_tau_module as M
+    if L != "0":
+        monkeypatch.setenv("PQD_MC_L", L)
+    rng = np.random.default_rng(10 + dim)
+    N2 = dim * dim
+    n_map, n_tb, nx_tau = 7, 12, 9
+    mk = lambda: np.eye(N2) + 0.05 * (rng.normal(size=(N2, N2)) + 1j * rng.normal(size=(N2, N2))) / dim  # noqa
+    dm_block = np.stack([mk() for _ in range(n_map)])
+    dm_s = mk()
+    time = np.round(np.arange(60) * 0.1, 6)
+    ts = np.array([0.0, 0.15, 0.4, 0.75, 1.1, 1.2, 1.25, 2.0, 3.3])
+    ops = [rng.normal(size=(dim, dim)) + 1j * rng.normal(size=(dim, dim)) for _ in range(3)]
+    rho = H.random_rho(dim).reshape(N2)
+    args = (F(dm_block), np.asfortranarray(dm_s), rho, n_tb, nx_tau, dim, *ops, time, ts)
+    a = M.calc_onetime_parallel_block(*args)
+    b = oracle.calc_onetime_parallel_block(*args)
+    assert rel(a, b) < 1e-11
+    monkeypatch.setenv("PQD_MC_BLOCKED", "0")
+    c = M.calc_onetime_parallel_block(*args)
+    assert rel(a, c) < 1e-11
+
+
 def test_mapchain_blocked_refuses_reads_past_the_maps():
     """a tau window running past the last map is refused (the Fortran would read past dm_tl)"""
     from pyaceqd_amd.two_time import propagate_tau_module as M
