@@ -94,8 +94,6 @@ struct SweepParams {
     int pt_mode;             // PT contraction: 0 VALU, 1 matrix cores (4x4x4_4b), 2 mixed per wave,
                              //   3 split-complex 16x16x4 (BT = 8), 4 matrix cores with 3 real products (3M)
     int cmul3;               // column phases with 3 real products per complex product (3M)
-    int col44;               // 3M column phases on v_mfma_f64_4x4x4_4b when N2 is not a multiple of 16 (PQD_COL44)
-    int variants;            // 1: a non-default switch above -> the A/B instance of the sweep kernel (pt_sweep_all.hip)
     const int4* units;       // 3M PT rows per wave: [waves][umax] (slice, row 0, row 1 or -1, row 2 | row 3 << 16 or -1;
                              //   a missing row 3 is 0x7FFF),
     int umax;                //   a unit with slice < 0 ends a wave's list; NULL: rows a = wave + k BT
@@ -211,7 +209,6 @@ constexpr int sweep_rmax(int N2, int BT, int CHI) {
     return N2 > 16 ? r : (r > 2 ? 2 : r);
 }
 hipError_t launch_sweep(int N2, int CHI, int BT, int n_blocks, const SweepParams& p, hipStream_t s);
-hipError_t launch_sweep_all(int N2, int CHI, int BT, int n_blocks, const SweepParams& p, hipStream_t s);
 int sweep_max_bt(int N2);
 hipError_t launch_sweep_nopt(int N2, int n_blocks, const SweepParams& p, hipStream_t s);
 hipError_t launch_mapchain(const MapChainParams& p, hipStream_t s);

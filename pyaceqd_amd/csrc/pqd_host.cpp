@@ -856,7 +856,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     if (P->quad) {
         const int nbq = (int)be.size();
         P->qcg = (nbq <= n_cu || (P->CHI == 32 && P->qpw == 1)) ? 2 : 4;
-        if (const char* e = getenv("PQD_QCG")) P->qcg = atoi(e) == 2 ? 2 : 4;
+        if (const char* e = getenv("PQD_QCG")) P->qcg = atoi(e) == 2 ? 2 : (atoi(e) == 1 && P->CHI == 32 ? 1 : 4);
         P->qpw = quad_qpw(P->CHI, P->qpw, P->qcg);
     }
     // trunk pre-pass instead of in-workgroup chains: every slot starts at its own branch step from a checkpoint
@@ -1001,9 +1001,8 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     // (six-level scan c5: 84.7 -> 79.5 ms per launch, profiles/r03/exp_c/c5_ptmode.log)
     { const char* pm = getenv("PQD_PT_MODE"); sp.pt_mode = pm ? atoi(pm) : (P->BT == 4 ? 5 : 4); }
     { const char* c3 = getenv("PQD_CMUL3"); sp.cmul3 = c3 ? atoi(c3) : 1; }
-    { const char* c4 = getenv("PQD_COL44"); sp.col44 = c4 ? atoi(c4) : 1; }
     { const char* tp = getenv("PQD_TRPRE"); sp.trpre = tp ? atoi(tp) : 1; }
-    if (pt && (sp.pt_mode == 4 || sp.pt_mode == 5 || sp.pt_mode == 6)) {
+    if (pt && (sp.pt_mode == 4 || sp.pt_mode == 5)) {
         const int nw = P->BT * sweep_wpt(P->N2, P->BT, P->CHI);
         int rmax = sweep_rmax(P->N2, P->BT, P->CHI);
         if (const char* e = getenv("PQD_ROWPAIR")) rmax = std::max(1, std::min(rmax, atoi(e) ? rmax : 1));
@@ -1012,11 +1011,6 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
         sp.units = P->units.p;
         sp.umax = (int)(u.size() / nw);
     }
-    // the production sweep instance holds the default variants only (3M rows from the unit list with one or two
-    // k-steps in flight, 3M columns on 4x4x4 tiles where N2 is not a multiple of 16); anything else runs the A/B
-    // instance (pt_sweep_all.hip)
-    sp.variants = !(sp.units && (sp.pt_mode == 4 || sp.pt_mode == 5) && sp.cmul3 == 1 &&
-                    (sp.col44 == 1 || N2 % 16 == 0)) ? 1 : 0;
     { const char* fz = getenv("PQD_FUSE"); sp.fuse = (!P->nopt && ns > 0 && (fz ? atoi(fz) : 1)) ? 1 : 0; }
     if (!sp.fuse) sp.trpre = 0;  // the prefetched rows are W(n), which exists only with fused half steps
     if (sp.fuse) {

@@ -74,7 +74,7 @@ __device__ __forceinline__ double2 quad_sum(double2 v) {  // sum over lanes l ^ 
 // NCG = 4-column groups per wave: 4 (strips of 16 columns, one wave per SIMD), 2 (strips of 8, twice the waves,
 // two per SIMD so one wave's LDS round trips and barrier hide behind the other's MFMAs)
 template <int CHI, int QPW, bool STAMP = false, int NCG = 4>
-__global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : 1) void pt_quad_kernel(SweepParams p) {
+__global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : (NCG == 1 ? 4 : 1)) void pt_quad_kernel(SweepParams p) {
     constexpr int CW = 4 * NCG;         // columns per wave
     constexpr int NWG = CHI / CW;       // waves per quad (column strips of CW)
     constexpr int KS = CHI / 4;         // k-steps of the contraction
@@ -538,7 +538,7 @@ bool quad_supported(int N2, int CHI) { return N2 == 4 && (CHI == 16 || CHI == 32
 
 // the instantiated quads per workgroup for a requested qpw: 1 or (chi = 16 with 16-column strips: 4 quads of one wave
 // each, a 256-thread workgroup) else 2
-int quad_qpw(int CHI, int qpw, int ncg) { return qpw <= 1 ? 1 : (CHI == 16 && ncg != 2 ? 4 : 2); }
+int quad_qpw(int CHI, int qpw, int ncg) { return (qpw <= 1 || ncg == 1) ? 1 : (CHI == 16 && ncg != 2 ? 4 : 2); }
 
 hipError_t launch_quad(int CHI, int n_quads, int qpw, int ncg, const SweepParams& p, hipStream_t s) {
     if (n_quads <= 0) return hipSuccess;
@@ -548,6 +548,8 @@ hipError_t launch_quad(int CHI, int n_quads, int qpw, int ncg, const SweepParams
             if (ncg == 2) return q == 2 ? launch_q<16, 2, 2>(n_quads, p, s) : launch_q<16, 1, 2>(n_quads, p, s);
             return q == 4 ? launch_q<16, 4, 4>(n_quads, p, s) : launch_q<16, 1, 4>(n_quads, p, s);
         case 32:
+            // ncg = 1 (4-column strips, 8 waves per quad, four waves per SIMD within 128 VGPRs): A/B only (PQD_QCG=1)
+            if (ncg == 1) return launch_q<32, 1, 1>(n_quads, p, s);
             if (ncg == 2) return q == 2 ? launch_q<32, 2, 2>(n_quads, p, s) : launch_q<32, 1, 2>(n_quads, p, s);
             return q == 2 ? launch_q<32, 2, 4>(n_quads, p, s) : launch_q<32, 1, 4>(n_quads, p, s);
         default: return hipErrorInvalidValue;

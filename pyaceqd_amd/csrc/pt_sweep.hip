@@ -166,53 +166,6 @@ __device__ __forceinline__ void col_apply_mfma3(const double2* __restrict__ Op, 
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
-// Column phase (3M) on v_mfma_f64_4x4x4_4b for N2 that is not a multiple of 16 (4, 9, 25, 36): 16x16 row tiles pad
-// N2 = 36 to 48 rows (25% of the column-phase MFMAs on zeros), 4-row tiles pad it to nothing (36) or little (9 -> 12,
-// 25 -> 28). The four blocks of one instruction are four 4-column groups of a 16-column tile sharing the operator
-// tile: lane l = 16 k + 4 blk + x holds Op[4 rt + x][4 kc + k] (A), S[4 kc + k][16 nt + (l & 15)] (B) and ends with
-// C[4 rt + (l >> 4)][16 nt + (l & 15)] (D) — the same LDS rows and columns the 16x16x4 path reads and writes. A wave
-// first reads its whole column tile (every k) into registers, so each row tile is written back as soon as it is done.
-template <int N2, int CHI, int RS, int WPT = 1>
-__device__ __forceinline__ void col_apply_mfma3_44(const double2* __restrict__ Op, double2* S, int lane, int half = 0) {
-    constexpr int KC = (N2 + 3) / 4;     // k chunks == row tiles
-    constexpr int NTL = CHI / 16;
-    const int x = lane & 3, kk = lane >> 4, c16 = lane & 15;
-    auto lda = [&](int rt, int kc) {
-        const int r = 4 * rt + x, a = 4 * kc + kk;
-        return (r < N2 && a < N2) ? Op[r * N2 + a] : c_zero();
-    };
-#pragma unroll 1
-    for (int j = 0; j < NTL / WPT; ++j) {
-        const int nt = j * WPT + half;
-        double2 b[KC];
-#pragma unroll
-        for (int kc = 0; kc < KC; ++kc) {
-            const int a = 4 * kc + kk;
-            b[kc] = (a < N2) ? S[a * RS + 16 * nt + c16] : c_zero();
-        }
-        // operator tile of row tile rt + 1 fetched element by element as row tile rt consumes its own
-        double2 an[KC];
-#pragma unroll
-        for (int kc = 0; kc < KC; ++kc) an[kc] = lda(0, kc);
-#pragma unroll 1
-        for (int rt = 0; rt < KC; ++rt) {
-            const int rn = rt + 1 < KC ? rt + 1 : rt;
-            double p1 = 0.0, p2 = 0.0, p3 = 0.0;
-#pragma unroll
-            for (int kc = 0; kc < KC; ++kc) {
-                const double2 a = an[kc];
-                an[kc] = lda(rn, kc);
-                p1 = __builtin_amdgcn_mfma_f64_4x4x4f64(a.x, b[kc].x, p1, 0, 0, 0);
-                p2 = __builtin_amdgcn_mfma_f64_4x4x4f64(a.y, b[kc].y, p2, 0, 0, 0);
-                p3 = __builtin_amdgcn_mfma_f64_4x4x4f64(a.x + a.y, b[kc].x + b[kc].y, p3, 0, 0, 0);
-            }
-            const int row = 4 * rt + kk;
-            if (row < N2) S[row * RS + 16 * nt + c16] = make_double2(p1 - p2, p3 - p1 - p2);
-        }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
-
 // PT contraction of one Liouville row alpha on the matrix cores (v_mfma_f64_4x4x4_4b_f64):
 //   C[BT x CHI] = X[BT x CHI] . Qg[CHI x CHI],  X = rows alpha of the BT trajectories.
 // gfx950 lane map of the 4-block f64 MFMA (measured): lane l = 16 k + 4 blk + x holds A[blk][x][k],
@@ -409,7 +362,7 @@ __device__ __forceinline__ void pt_row_mfma16(const double2* __restrict__ Qg, do
 // Reads every half step's M, F, W as stored: plans running this kernel (main sweep or trunk pre-pass) build the free
 // propagators without pulse windows (pqd_host.cpp). A window-select form of these loads measured 1.8% slower on the
 // bench launch even with its selects folded away at compile time (202.3 vs 198.1 ms, profiles/r02/windows/).
-template <int N2, int CHI, int BT, bool TRUNK, bool ALL>
+template <int N2, int CHI, int BT, bool TRUNK>
 __global__ __launch_bounds__(64 * BT * sweep_wpt(N2, BT, CHI)) void pt_sweep_kernel(SweepParams p, const double2* __restrict__ Mg,
                                                            const double2* __restrict__ Qg0, double2* __restrict__ outg,
                                                            const double2* __restrict__ Fg, const double2* __restrict__ Wg) {
@@ -476,28 +429,9 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(N2, BT, CHI)) void pt_sweep_ker
     // waves per trajectory the column tiles of half w / BT
     double2* stw = st + tw * TS;
     const bool c3 = p.cmul3 != 0;
-    const bool c44 = p.col44 != 0;
-    // ALL = false (the production instance) holds the default column product only (3M; 4x4x4 tiles when N2 is not a
-    // multiple of 16); the A/B switches (4M, 16x16 tiles at such N2) live in the ALL = true instance, so their
-    // registers do not weigh on the default path
     auto col = [&](const double2* __restrict__ Op) {
-        if constexpr (!ALL) {
-#ifndef PQD_PROD_COL16
-            if constexpr (N2 % 16 != 0) col_apply_mfma3_44<N2, CHI, RS, WPT>(Op, stw, lane, half);
-            else col_apply_mfma3<N2, CHI, RS, WPT>(Op, stw, lane, half);
-#else
-            col_apply_mfma3<N2, CHI, RS, WPT>(Op, stw, lane, half);  // A/B build: 16x16 tiles everywhere
-#endif
-        } else {
-            if constexpr (N2 % 16 != 0) {
-                if (c3 && c44) {
-                    col_apply_mfma3_44<N2, CHI, RS, WPT>(Op, stw, lane, half);
-                    return;
-                }
-            }
-            if (c3) col_apply_mfma3<N2, CHI, RS, WPT>(Op, stw, lane, half);
-            else col_apply_mfma<N2, CHI, RS, WPT>(Op, stw, lane, half);
-        }
+        if (c3) col_apply_mfma3<N2, CHI, RS, WPT>(Op, stw, lane, half);
+        else col_apply_mfma<N2, CHI, RS, WPT>(Op, stw, lane, half);
     };
     int ev_cur = 0, ev_lim = 0;
     {
@@ -656,20 +590,17 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(N2, BT, CHI)) void pt_sweep_ker
             // complex product (default), 3: split-complex 16x16x4 rows (BT = 8), 2: mixed (waves 0..NW/2-1 start on the matrix cores,
             // the others on the VALU, alternating per row), so the two FP64 pipes of a SIMD run concurrently
             int parity = (p.pt_mode == 2) ? ((wave >= NW / 2) ? 1 : 0) : 0;
-            if (p.units && (p.pt_mode == 4 || p.pt_mode == 5 || p.pt_mode == 6)) {
-                // 3M rows by the host's per-wave unit list: (slice, row 0, row 1 or -1, rows 2 | 3 << 16 or -1);
-                // modes 5 / 6 keep 2 / 3 k-steps of the slice in flight (BT = 4: half the MFMAs per k-step of BT = 8,
-                // so the L2 latency needs a deeper prefetch)
+            if (p.units && (p.pt_mode == 4 || p.pt_mode == 5)) {
+                // 3M rows by the host's per-wave unit list: (slice, row 0, row 1 or -1, rows 2 | 3 << 16 or -1)
                 const int4* U = p.units + (size_t)wave * p.umax;
                 for (int u = 0; u < p.umax; ++u) {
                     const int4 e = U[u];
                     if (e.x < 0) break;
                     const double2* Qg = Qs + (size_t)e.x * CHI * CHI;
                     if (p.pt_mode == 5) pt_rows3<N2, CHI, BT, RS, TS, 2>(Qg, st, e, lane);
-                    else if (ALL && BT == 4 && p.pt_mode == 6) pt_rows3<N2, CHI, BT, RS, TS, 3>(Qg, st, e, lane);
                     else pt_rows3<N2, CHI, BT, RS, TS, 1>(Qg, st, e, lane);
                 }
-            } else if constexpr (ALL)
+            } else
             for (int a = wave; a < N2; a += NW) {
                 const double2* Qg = Qs + (size_t)p.gmap[a] * CHI * CHI;
                 const bool use_mfma = (p.pt_mode == 1) || (p.pt_mode == 2 && parity == 0);
@@ -848,78 +779,38 @@ __global__ __launch_bounds__(64) void sweep_nopt_kernel(SweepParams p) {
     }
 }
 
-template <int N2, int CHI, int BT, bool TRUNK, bool ALL>
+template <int N2, int CHI, int BT, bool TRUNK>
 hipError_t launch_sw(int n_blocks, const SweepParams& p, hipStream_t s) {
     using L = SweepLayout<N2, CHI, BT>;
     static_assert(L::LDS <= 160 * 1024, "LDS budget");
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)pt_sweep_kernel<N2, CHI, BT, TRUNK, ALL>,
+        hipError_t e = hipFuncSetAttribute((const void*)pt_sweep_kernel<N2, CHI, BT, TRUNK>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::LDS);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((pt_sweep_kernel<N2, CHI, BT, TRUNK, ALL>), dim3(n_blocks), dim3(64 * L::NW), L::LDS, s, p, p.M,
-                       p.Q, p.out, p.F, p.W);
+    hipLaunchKernelGGL((pt_sweep_kernel<N2, CHI, BT, TRUNK>), dim3(n_blocks), dim3(64 * L::NW), L::LDS, s, p, p.M, p.Q,
+                       p.out, p.F, p.W);
     return hipGetLastError();
 }
 
-template <int N2, int BT, bool TRUNK, bool ALL>
+template <int N2, int BT, bool TRUNK = false>
 hipError_t launch_sw_chi(int CHI, int n_blocks, const SweepParams& p, hipStream_t s) {
     switch (CHI) {
-        case 16: return launch_sw<N2, 16, BT, TRUNK, ALL>(n_blocks, p, s);
-        case 32: return launch_sw<N2, 32, BT, TRUNK, ALL>(n_blocks, p, s);
-        case 64: return launch_sw<N2, 64, BT, TRUNK, ALL>(n_blocks, p, s);
+        case 16: return launch_sw<N2, 16, BT, TRUNK>(n_blocks, p, s);
+        case 32: return launch_sw<N2, 32, BT, TRUNK>(n_blocks, p, s);
+        case 64: return launch_sw<N2, 64, BT, TRUNK>(n_blocks, p, s);
         case 128:
             // chi = 128 keeps 4 augmented states of N2 <= 16 in LDS (132 KiB); larger N2 or BT do not fit
-            if constexpr (BT == 4 && N2 <= 16) return launch_sw<N2, 128, BT, TRUNK, ALL>(n_blocks, p, s);
+            if constexpr (BT == 4 && N2 <= 16) return launch_sw<N2, 128, BT, TRUNK>(n_blocks, p, s);
             return hipErrorInvalidValue;
-        default: return hipErrorInvalidValue;
-    }
-}
-
-template <bool ALL>
-hipError_t launch_sweep_t(int N2, int CHI, int BT, int n_blocks, const SweepParams& p, hipStream_t s) {
-    if (n_blocks <= 0) return hipSuccess;
-    if (p.ck_map) {  // trunk pre-pass: four trunks per workgroup
-        if (BT != 4) return hipErrorInvalidValue;
-        switch (N2) {
-            case 4: return launch_sw_chi<4, 4, true, ALL>(CHI, n_blocks, p, s);
-            case 9: return launch_sw_chi<9, 4, true, ALL>(CHI, n_blocks, p, s);
-            case 16: return launch_sw_chi<16, 4, true, ALL>(CHI, n_blocks, p, s);
-            case 25: return launch_sw_chi<25, 4, true, ALL>(CHI, n_blocks, p, s);
-            case 36: return launch_sw_chi<36, 4, true, ALL>(CHI, n_blocks, p, s);
-            default: return hipErrorInvalidValue;
-        }
-    }
-    if (BT == 8) {
-        switch (N2) {
-            case 4: return launch_sw_chi<4, 8, false, ALL>(CHI, n_blocks, p, s);
-            case 9: return launch_sw_chi<9, 8, false, ALL>(CHI, n_blocks, p, s);
-            case 16: return launch_sw_chi<16, 8, false, ALL>(CHI, n_blocks, p, s);
-            default: return hipErrorInvalidValue;
-        }
-    }
-    if (BT != 4) return hipErrorInvalidValue;
-    switch (N2) {
-        case 4: return launch_sw_chi<4, 4, false, ALL>(CHI, n_blocks, p, s);
-        case 9: return launch_sw_chi<9, 4, false, ALL>(CHI, n_blocks, p, s);
-        case 16: return launch_sw_chi<16, 4, false, ALL>(CHI, n_blocks, p, s);
-        case 25: return launch_sw_chi<25, 4, false, ALL>(CHI, n_blocks, p, s);
-        case 36: return launch_sw_chi<36, 4, false, ALL>(CHI, n_blocks, p, s);
         default: return hipErrorInvalidValue;
     }
 }
 
 }  // namespace
 
-#ifdef PQD_SWEEP_ALL_TU
-// pt_sweep_all.hip: the sweep kernel with every A/B switch compiled in (PQD_PT_MODE other than 4 / 5, PQD_CMUL3=0,
-// PQD_COL44=0), a translation unit of its own so the two instances build in parallel
-hipError_t launch_sweep_all(int N2, int CHI, int BT, int n_blocks, const SweepParams& p, hipStream_t s) {
-    return launch_sweep_t<true>(N2, CHI, BT, n_blocks, p, s);
-}
-#else
 bool sweep_supported(int N2, int CHI) {
     return (N2 == 4 || N2 == 9 || N2 == 16 || N2 == 25 || N2 == 36) &&
            (CHI == 1 || CHI == 16 || CHI == 32 || CHI == 64 || (CHI == 128 && N2 <= 16));
@@ -929,8 +820,35 @@ bool sweep_supported(int N2, int CHI) {
 int sweep_max_bt(int N2) { return N2 <= 16 ? 8 : 4; }
 
 hipError_t launch_sweep(int N2, int CHI, int BT, int n_blocks, const SweepParams& p, hipStream_t s) {
-    if (p.variants) return launch_sweep_all(N2, CHI, BT, n_blocks, p, s);
-    return launch_sweep_t<false>(N2, CHI, BT, n_blocks, p, s);
+    if (n_blocks <= 0) return hipSuccess;
+    if (p.ck_map) {  // trunk pre-pass: four trunks per workgroup
+        if (BT != 4) return hipErrorInvalidValue;
+        switch (N2) {
+            case 4: return launch_sw_chi<4, 4, true>(CHI, n_blocks, p, s);
+            case 9: return launch_sw_chi<9, 4, true>(CHI, n_blocks, p, s);
+            case 16: return launch_sw_chi<16, 4, true>(CHI, n_blocks, p, s);
+            case 25: return launch_sw_chi<25, 4, true>(CHI, n_blocks, p, s);
+            case 36: return launch_sw_chi<36, 4, true>(CHI, n_blocks, p, s);
+            default: return hipErrorInvalidValue;
+        }
+    }
+    if (BT == 8) {
+        switch (N2) {
+            case 4: return launch_sw_chi<4, 8>(CHI, n_blocks, p, s);
+            case 9: return launch_sw_chi<9, 8>(CHI, n_blocks, p, s);
+            case 16: return launch_sw_chi<16, 8>(CHI, n_blocks, p, s);
+            default: return hipErrorInvalidValue;
+        }
+    }
+    if (BT != 4) return hipErrorInvalidValue;
+    switch (N2) {
+        case 4: return launch_sw_chi<4, 4>(CHI, n_blocks, p, s);
+        case 9: return launch_sw_chi<9, 4>(CHI, n_blocks, p, s);
+        case 16: return launch_sw_chi<16, 4>(CHI, n_blocks, p, s);
+        case 25: return launch_sw_chi<25, 4>(CHI, n_blocks, p, s);
+        case 36: return launch_sw_chi<36, 4>(CHI, n_blocks, p, s);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_sweep_nopt(int N2, int n_traj, const SweepParams& p, hipStream_t s) {
@@ -943,4 +861,3 @@ hipError_t launch_sweep_nopt(int N2, int n_traj, const SweepParams& p, hipStream
 #undef PQD_NOPT
     return hipGetLastError();
 }
-#endif

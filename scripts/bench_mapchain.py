@@ -60,14 +60,15 @@ def case_onetime(dim, n_t=256, n_tau=10000, reps=5, cpu=True):
     el, got = _time(lambda: gpu.calc_onetime_parallel(*args), reps)
     row = {"case": f"onetime_d{dim}", "n_t": n_t, "n_tau": n_tau, "N2": dim * dim, "gpu_wall_s": el,
            "gpu_traj_steps_per_s": n_t * n_tau / el}
-    if cpu:
+
+    def cpu_part():
         from oracle import fref
         if fref.available():
             elc, ref = _time(lambda: fref.calc_onetime_parallel(*args), 3)
             row.update(cpu_ref_wall_s=elc, cpu_ref_traj_steps_per_s=n_t * n_tau / elc,
                        max_rel_diff=float(np.max(np.abs(got - ref)) / np.max(np.abs(ref))),
                        speedup=elc / el)
-    return row
+    return row, (cpu_part if cpu else None)
 
 
 def case_block(dim=4, n_t=256, n_tb=100, nx_tau=100, reps=5, cpu=True):
@@ -86,13 +87,14 @@ def case_block(dim=4, n_t=256, n_tb=100, nx_tau=100, reps=5, cpu=True):
     steps = n_t * n_tb * nx_tau
     row = {"case": f"block_d{dim}", "n_t": n_t, "tau_steps": n_tb * nx_tau, "gpu_wall_s": el,
            "gpu_traj_steps_per_s": steps / el}
-    if cpu:
+
+    def cpu_part():
         from oracle import fref
         if fref.available():
             elc, ref = _time(lambda: fref.calc_onetime_parallel_block(*args), 3)
             row.update(cpu_ref_wall_s=elc, cpu_ref_traj_steps_per_s=steps / elc,
                        max_rel_diff=float(np.max(np.abs(got - ref)) / np.max(np.abs(ref))), speedup=elc / el)
-    return row
+    return row, (cpu_part if cpu else None)
 
 
 def case_ft8(dim=4, n_t=128, reps=3, cpu=True):
@@ -110,14 +112,15 @@ def case_ft8(dim=4, n_t=128, reps=3, cpu=True):
     fn = lambda: gpu.four_time_8op(dm1, dm2, rho0, t1, precalc, dt, dim, *ops8, False, False, tb)  # noqa: E731
     el, got = _time(fn, reps)
     row = {"case": f"four_time_8op_d{dim}", "n_t": n_t, "pairs": n_t * (n_t + 1) // 2, "gpu_wall_s": el}
-    if cpu:
+
+    def cpu_part():
         from oracle import fref
         if fref.available():
             elc, ref = _time(lambda: fref.four_time_8op(dm1, dm2, rho0, t1, precalc, dt, dim, ops8, False, False,
                                                         tb), 3)
             row.update(cpu_ref_wall_s=elc, max_rel_diff=float(np.max(np.abs(got - ref)) / np.max(np.abs(ref))),
                        speedup=elc / el)
-    return row
+    return row, (cpu_part if cpu else None)
 
 
 def case_tlmap(n_maps=4000, N2=16, reps=3, cpu=True):
@@ -126,13 +129,14 @@ def case_tlmap(n_maps=4000, N2=16, reps=3, cpu=True):
     times = 0.1 * np.arange(n_maps + 1)
     el, got = _time(lambda: tools.calc_tl_dynmap_pseudo(dm, times), reps)
     row = {"case": f"tl_dynmap_N2_{N2}", "maps": n_maps, "gpu_wall_s": el, "maps_per_s": n_maps / el}
-    if cpu:
+
+    def cpu_part():
         t0 = time.perf_counter()
         ref = [dm[0]] + [dm[i] @ np.linalg.pinv(dm[i - 1], rcond=1e-12) for i in range(1, n_maps)]
         elc = time.perf_counter() - t0
         row.update(cpu_numpy_wall_s=elc, speedup=elc / el,
                    max_rel_diff=float(max(np.max(np.abs(a - b)) for a, b in zip(got, ref))))
-    return row
+    return row, (cpu_part if cpu else None)
 
 
 def main():
@@ -143,16 +147,23 @@ def main():
     args = ap.parse_args()
     os.environ.setdefault("OMP_NUM_THREADS", str(args.cpu_threads))
     cpu = not args.no_cpu
+    # every GPU timing first, then the CPU references: the reference's OpenMP threads keep spinning for a while
+    # after each call (libomp blocktime) and would take cores from the GPU calls' host side
+    done = []
     for c in args.cases.split(","):
         if c == "onetime":
             for d in (2, 4, 6):
-                print(json.dumps(case_onetime(d, cpu=cpu)), flush=True)
+                done.append(case_onetime(d, cpu=cpu))
         elif c == "block":
-            print(json.dumps(case_block(cpu=cpu)), flush=True)
+            done.append(case_block(cpu=cpu))
         elif c == "ft8":
-            print(json.dumps(case_ft8(cpu=cpu)), flush=True)
+            done.append(case_ft8(cpu=cpu))
         elif c == "tlmap":
-            print(json.dumps(case_tlmap(cpu=cpu)), flush=True)
+            done.append(case_tlmap(cpu=cpu))
+    for row, cpu_part in done:
+        if cpu_part is not None:
+            cpu_part()
+        print(json.dumps(row), flush=True)
 
 
 if __name__ == "__main__":

@@ -27,7 +27,7 @@ def _run(systems, grid, rho0, ops, tr, pt):
 @pytest.mark.parametrize("chi", [8, 16, 32])
 @pytest.mark.parametrize("fuse", ["0", "1"])
 @pytest.mark.parametrize("qpw", ["1", "2"])
-@pytest.mark.parametrize("qcg", ["2", "4"])
+@pytest.mark.parametrize("qcg", ["1", "2", "4"])
 def test_quad_vs_oracle(monkeypatch, chi, fuse, qpw, qcg):
     monkeypatch.setenv("PQD_FUSE", fuse)
     monkeypatch.setenv("PQD_QPW", qpw)
@@ -77,7 +77,7 @@ def _g2_sweep(n_t1, n_tau, seed):
 
 
 @pytest.mark.parametrize("mode", ["branch", "trunk", "none"])
-@pytest.mark.parametrize("qcg", ["2", "4"])
+@pytest.mark.parametrize("qcg", ["1", "2", "4"])
 def test_quad_shared_trunks(monkeypatch, mode, qcg):
     monkeypatch.setenv("PQD_QCG", qcg)
     monkeypatch.setenv("PQD_SPLIT", "0")
