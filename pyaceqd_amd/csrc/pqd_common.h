@@ -105,6 +105,8 @@ struct SweepParams {
     int traj_base;           // split groups: trajectory of group 0 (a batch run as several co-resident launches)
     int n_steps;             // grid steps (operand prefetch bound)
     int n_blk;               // blocks of the launch (quad kernel: quads; tail workgroups check it)
+    int qprio;               // quad kernel wave priorities (PQD_QPRIO, A/B): bit 0 first half of the grid above the
+                             //   second, bit 1 raised outside the PT contraction
     const int2* win;         // per-system pulse windows (FreePropParams::win) or NULL; outside them M, F, W are the
     const double2* Midle;    //   system's idle operators: Midle [n_sys][N2 x N2], Fidle = Midle Midle [n_sys][N2 x N2],
     const double2* Fidle;    //   Widle = ovec . Midle [n_sys][n_out][N2]

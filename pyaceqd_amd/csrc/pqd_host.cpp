@@ -810,7 +810,10 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     // PQD_QUAD=0 (A/B); its blocks are quads
     {
         const char* e = getenv("PQD_QUAD");
-        P->quad = pt && !P->split && quad_supported(N2, P->CHI) && !(e && atoi(e) == 0);
+        // chi = 64 quads only on request (PQD_QUAD=2): their slices do not fit the registers yet and the batched
+        // kernel is faster (C2 shape at chi = 64: 19.9 ms batched, 41.9 ms quads; profiles/r03/q64.log)
+        P->quad = pt && !P->split && quad_supported(N2, P->CHI) && !(e && atoi(e) == 0) &&
+                  (P->CHI != 64 || (e && atoi(e) == 2));
         // chi = 32: one quad per workgroup, so the two 8-column-strip workgroups sharing a CU barrier independently
         // (C2: 19.8 -> 18.4 ms per launch with the strips below, profiles/r02/quad/envab_qpw_qcg.log)
         if (P->CHI == 32) P->qpw = 1;
@@ -1030,6 +1033,11 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     sp.woff = P->woff.p; sp.ev_start = P->ev_start.p; sp.ev = P->ev.p; sp.sop = P->sop.p; sp.out = P->out.p;
     sp.n_steps = ns;
     sp.n_blk = nb;
+    // quad kernel: waves raise their priority outside the PT contraction, so a wave on its serial chain (column
+    // operator, exchange, relayout) issues ahead of the other quad's MFMA stream on the same SIMD (C2: 17.5 -> 16.1 ms;
+    // a static bias between the grid halves gains nothing; profiles/r03/quad_prio.log)
+    sp.qprio = 2;
+    if (const char* e = getenv("PQD_QPRIO")) sp.qprio = atoi(e) & 3;
     finalize_trunks(P);
     if (P->split) {
         HIPCHK(P->Xs.alloc((size_t)P->n_traj * 2 * N2 * P->CHI));
@@ -1346,6 +1354,14 @@ static int mapchain_run(pqd_ctx* ctx, MapChainParams& p, const pqd_c128* dmA, si
     const bool tmg = getenv("PQD_MC_TIMING") != nullptr;
     auto now = [] { return std::chrono::steady_clock::now(); };
     const auto t0 = now();
+    // the caller's result array is typically fresh (f2py-style: np.zeros, pages not yet mapped): fault its pages in
+    // on a few host threads while the maps upload and the kernels run, so the copy back runs at the link rate (a
+    // 41 MB copy into fresh pages: 1.7 ms, into mapped ones 0.73 ms; scripts/ubench_h2d.py)
+    std::thread toucher(touch_pages, (void*)result, nres * sizeof(double2));
+    struct Join {
+        std::thread& t;
+        ~Join() { if (t.joinable()) t.join(); }
+    } join_toucher{toucher};
     HIPCHK(up(p.dmA, dmA, nA * m2 * sizeof(double2)));
     if (dmB) HIPCHK(up(p.dmB, dmB, nB * m2 * sizeof(double2)));
     if (dmT) HIPCHK(up(p.dmT, dmT, nT * m2 * sizeof(double2)));
@@ -1364,11 +1380,8 @@ static int mapchain_run(pqd_ctx* ctx, MapChainParams& p, const pqd_c128* dmA, si
         HIPCHK(hipMemsetAsync(p.result, 0, nres * sizeof(double2), s));
         HIPCHK(launch_mapchain(p, s));
     }
-    // the caller's result array is typically fresh (f2py-style: np.zeros, pages not yet mapped): fault its pages in
-    // on a few host threads while the kernels run, so the copy back runs at the link rate (a 41 MB copy into fresh
-    // pages: 2.4 ms, into mapped ones 0.76 ms; scripts/ubench_h2d.py)
     const auto t1 = now();
-    touch_pages(result, nres * sizeof(double2));
+    toucher.join();
     const auto t2 = now();
     if (tmg) HIPCHK(hipStreamSynchronize(s));
     const auto t3 = now();
@@ -1377,7 +1390,7 @@ static int mapchain_run(pqd_ctx* ctx, MapChainParams& p, const pqd_c128* dmA, si
     if (tmg) {
         const auto t4 = now();
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        fprintf(stderr, "pqd mapchain: upload+launch %.3f ms, page touch %.3f ms, kernels left %.3f ms, download %.3f ms\n",
+        fprintf(stderr, "pqd mapchain: upload+launch %.3f ms, page touch left %.3f ms, kernels left %.3f ms, download %.3f ms\n",
                 ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, t4));
     }
     return PQD_OK;

@@ -30,6 +30,10 @@
 #include <cstdlib>
 #include <type_traits>
 
+#ifndef PQD_QRAISE
+#define PQD_QRAISE(KS) (KS)
+#endif
+
 namespace {
 
 __device__ __forceinline__ double mfma4(double a, double b, double c) {
@@ -55,6 +59,14 @@ __device__ __forceinline__ void quad_col(double2 a, bool mine, double2 (&R)[NCG]
 // diagnostics (PQD_ABLATE bit 32, scripts/quad_stamps.py): s_memtime at the phase boundaries of steps
 // 1000..1015, workgroup 0, wave 0 (a separate instantiation; the production kernel carries none of it)
 __device__ unsigned long long g_quad_stamps[16 * 16];
+
+// s_setprio takes an immediate
+__device__ __forceinline__ void set_prio(int k) {
+    if (k <= 0) __builtin_amdgcn_s_setprio(0);
+    else if (k == 1) __builtin_amdgcn_s_setprio(1);
+    else if (k == 2) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(3);
+}
 
 // DPP lane exchange inside groups of four lanes (quad_perm), on a double's two halves: no LDS round trip
 template <int CTRL>
@@ -129,6 +141,9 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : (NCG =
     __syncthreads();
     const int n_lo = s_lo, n_hi = s_hi;
     if (n_hi < 0 || n_lo == INT_MAX) return;  // whole workgroup empty
+    const int pbase = (p.qprio & 1) && 2 * (int)blockIdx.x < (int)gridDim.x ? 1 : 0;
+    const bool pdyn = (p.qprio & 2) != 0;
+    if (p.qprio) set_prio(pbase + (pdyn ? 2 : 0));
 
     double2* stq = smem + q * QST;        // + parity * QPW * QST
     const int crow = (4 * lt + la) * RS + CW * h + lc;                     // C-layout element (+ 4 cg)
@@ -445,12 +460,14 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : (NCG =
         else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         stamp(2);
         // contraction of step n
+        if (pdyn) set_prio(pbase);
         double2 A[KS];
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) A[ks] = st[arow + 4 * ks];
         double p1[NCG] = {}, p2[NCG] = {}, p3[NCG] = {};
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
+            if (ks == PQD_QRAISE(KS) && pdyn) set_prio(pbase + 2);
             const double as = A[ks].x + A[ks].y;
 #pragma unroll
             for (int cg = 0; cg < NCG; ++cg) {
@@ -459,6 +476,9 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : (NCG =
                 p3[cg] = mfma4(as, PRESUM ? Bs[PRESUM ? ks : 0][PRESUM ? cg : 0] : B[ks][cg].x + B[ks][cg].y, p3[cg]);
             }
         }
+        // priority raised again once the MFMAs are issued: the traces, the relayout and the next column operator
+        // are the serial chain (C2: 16.0 -> 15.8 ms against raising it after the results, profiles/r03/quad_prio.log)
+        if (PQD_QRAISE(KS) >= KS && pdyn) set_prio(pbase + 2);
         // traces of step n (strip 0; every slot is fused: W(n) rows), stored inside each trajectory's window
         if (h == 0) {
             double2 r = rpp[4 * t2 + a2];
@@ -534,11 +554,13 @@ extern "C" int pqd_debug_quad_stamps(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_quad_stamps), sizeof(unsigned long long) * 256) == hipSuccess ? 0 : 4;
 }
 
-bool quad_supported(int N2, int CHI) { return N2 == 4 && (CHI == 16 || CHI == 32); }
+bool quad_supported(int N2, int CHI) { return N2 == 4 && (CHI == 16 || CHI == 32 || CHI == 64); }
 
-// the instantiated quads per workgroup for a requested qpw: 1 or (chi = 16 with 16-column strips: 4 quads of one wave
-// each, a 256-thread workgroup) else 2
-int quad_qpw(int CHI, int qpw, int ncg) { return (qpw <= 1 || ncg == 1) ? 1 : (CHI == 16 && ncg != 2 ? 4 : 2); }
+// the instantiated quads per workgroup for a requested qpw: 1 (always at chi = 64) or (chi = 16 with 16-column strips:
+// 4 quads of one wave each, a 256-thread workgroup) else 2
+int quad_qpw(int CHI, int qpw, int ncg) {
+    return (qpw <= 1 || ncg == 1 || CHI == 64) ? 1 : (CHI == 16 && ncg != 2 ? 4 : 2);
+}
 
 hipError_t launch_quad(int CHI, int n_quads, int qpw, int ncg, const SweepParams& p, hipStream_t s) {
     if (n_quads <= 0) return hipSuccess;
@@ -552,6 +574,9 @@ hipError_t launch_quad(int CHI, int n_quads, int qpw, int ncg, const SweepParams
             if (ncg == 1) return launch_q<32, 1, 1>(n_quads, p, s);
             if (ncg == 2) return q == 2 ? launch_q<32, 2, 2>(n_quads, p, s) : launch_q<32, 1, 2>(n_quads, p, s);
             return q == 2 ? launch_q<32, 2, 4>(n_quads, p, s) : launch_q<32, 1, 4>(n_quads, p, s);
+        case 64:
+            // one quad per workgroup: 8-column strips (eight waves, two per SIMD) or 16-column strips (four waves)
+            return ncg == 4 ? launch_q<64, 1, 4>(n_quads, p, s) : launch_q<64, 1, 2>(n_quads, p, s);
         default: return hipErrorInvalidValue;
     }
 }

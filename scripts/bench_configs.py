@@ -107,6 +107,7 @@ CONFIGS = {
     "c2": dict(model="tls", n_scan=2048, n_t1=1, n_tau=10000, chi=32),
     "c3one": dict(model="biexciton", n_scan=1, n_t1=1, n_tau=10000, chi=64),
     "c2one": dict(model="tls", n_scan=1, n_t1=1, n_tau=10000, chi=32),
+    "c2x64": dict(model="tls", n_scan=2048, n_t1=1, n_tau=10000, chi=64),
     "c5one": dict(model="sixls", n_scan=1, n_t1=1, n_tau=10000, chi=64),
     "c3eight": dict(model="biexciton", n_scan=8, n_t1=1, n_tau=10000, chi=64),
     "c3twenty": dict(model="biexciton", n_scan=20, n_t1=1, n_tau=10000, chi=64),

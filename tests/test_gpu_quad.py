@@ -24,7 +24,7 @@ def _run(systems, grid, rho0, ops, tr, pt):
     return got, plan.info()[0]
 
 
-@pytest.mark.parametrize("chi", [8, 16, 32])
+@pytest.mark.parametrize("chi", [8, 16, 32, 64])
 @pytest.mark.parametrize("fuse", ["0", "1"])
 @pytest.mark.parametrize("qpw", ["1", "2"])
 @pytest.mark.parametrize("qcg", ["1", "2", "4"])
@@ -33,6 +33,8 @@ def test_quad_vs_oracle(monkeypatch, chi, fuse, qpw, qcg):
     monkeypatch.setenv("PQD_QPW", qpw)
     monkeypatch.setenv("PQD_QCG", qcg)
     monkeypatch.setenv("PQD_SPLIT", "0")
+    if chi == 64:
+        monkeypatch.setenv("PQD_QUAD", "2")  # chi = 64 quads are opt-in
     N = 2
     systems = [H.random_system(N, n_steps=40, seed=60 + k)[0] for k in range(3)]
     grid = Grid(0.0, 0.1, 40)
