@@ -111,6 +111,7 @@ struct SweepParams {
     const double2* Midle;    //   system's idle operators: Midle [n_sys][N2 x N2], Fidle = Midle Midle [n_sys][N2 x N2],
     const double2* Fidle;    //   Widle = ovec . Midle [n_sys][n_out][N2]
     const double2* Widle;
+    int colbig;              // N2 > 16 column phases: one pass over k for all of a wave's tiles (1, PQD_COLBIG; 0: per tile)
 };
 
 // ---- free propagators through the pulse windows: M(h), F(n) = M(2n) M(2n-1) and W(n) = ovec . M(2n-1) of system sys

@@ -1005,6 +1005,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     { const char* pm = getenv("PQD_PT_MODE"); sp.pt_mode = pm ? atoi(pm) : (P->BT == 4 ? 5 : 4); }
     { const char* c3 = getenv("PQD_CMUL3"); sp.cmul3 = c3 ? atoi(c3) : 1; }
     { const char* tp = getenv("PQD_TRPRE"); sp.trpre = tp ? atoi(tp) : 1; }
+    { const char* cb = getenv("PQD_COLBIG"); sp.colbig = cb ? atoi(cb) : 1; }
     if (pt && (sp.pt_mode == 4 || sp.pt_mode == 5)) {
         const int nw = P->BT * sweep_wpt(P->N2, P->BT, P->CHI);
         int rmax = sweep_rmax(P->N2, P->BT, P->CHI);

@@ -166,6 +166,74 @@ __device__ __forceinline__ void col_apply_mfma3(const double2* __restrict__ Op, 
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
+// col_apply_mfma3 for large N2 (25, 36: the operator's fragments do not fit in VGPRs): all of this wave's column tiles
+// in one pass over k, so every operator fragment is loaded from L2 once per call instead of once per tile, with the
+// next k-step's fragments in flight while the current one's MFMAs run (the per-tile loop waited on each load:
+// six-level scan, column phases ~24 us per step against ~9 us of MFMA work). Accumulators: 3 MT NTW tiles <= 18.
+template <int N2, int CHI, int RS, int WPT>
+constexpr bool col_big_ok() {
+    return (N2 + 3) / 4 * ((N2 + 15) / 16) > 8 && 3 * ((N2 + 15) / 16) * (CHI / 16 / WPT) <= 18;
+}
+template <int N2, int CHI, int RS, int WPT>
+__device__ __forceinline__ void col_apply_mfma3_big(const double2* __restrict__ Op, double2* S, int lane, int half) {
+    constexpr int MT = (N2 + 15) / 16;
+    constexpr int KS = (N2 + 3) / 4;
+    constexpr int NTW = CHI / 16 / WPT;   // this wave's column tiles: half, half + WPT, ...
+    const int li = lane & 15, lk = lane >> 4;
+    dbl4 p1[MT][NTW], p2[MT][NTW], p3[MT][NTW];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) { p1[mt][j] = dbl4{0, 0, 0, 0}; p2[mt][j] = p1[mt][j]; p3[mt][j] = p1[mt][j]; }
+    auto ldm = [&](int ks, int mt) {
+        const int r = 16 * mt + li, a = 4 * ks + lk;
+        return (r < N2 && a < N2) ? Op[r * N2 + a] : c_zero();
+    };
+    double2 mn[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) mn[mt] = ldm(0, mt);
+#pragma unroll 3
+    for (int ks = 0; ks < KS; ++ks) {
+        double2 m[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) m[mt] = mn[mt];
+        if (ks + 1 < KS) {
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) mn[mt] = ldm(ks + 1, mt);
+        }
+        const int a = 4 * ks + lk;
+        double2 b[NTW];
+        double bs[NTW];
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+            b[j] = (a < N2) ? S[a * RS + 16 * (j * WPT + half) + li] : c_zero();
+            bs[j] = b[j].x + b[j].y;
+        }
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            const double ms = m[mt].x + m[mt].y;
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) {
+                p1[mt][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(m[mt].x, b[j].x, p1[mt][j], 0, 0, 0);
+                p2[mt][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(m[mt].y, b[j].y, p2[mt][j], 0, 0, 0);
+                p3[mt][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(ms, bs[j], p3[mt][j], 0, 0, 0);
+            }
+        }
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int j = 0; j < NTW; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 16 * mt + lk + 4 * r;
+                if (row < N2)
+                    S[row * RS + 16 * (j * WPT + half) + li] =
+                        make_double2(p1[mt][j][r] - p2[mt][j][r], p3[mt][j][r] - p1[mt][j][r] - p2[mt][j][r]);
+            }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
 // PT contraction of one Liouville row alpha on the matrix cores (v_mfma_f64_4x4x4_4b_f64):
 //   C[BT x CHI] = X[BT x CHI] . Qg[CHI x CHI],  X = rows alpha of the BT trajectories.
 // gfx950 lane map of the 4-block f64 MFMA (measured): lane l = 16 k + 4 blk + x holds A[blk][x][k],
@@ -429,9 +497,16 @@ __global__ __launch_bounds__(64 * BT * sweep_wpt(N2, BT, CHI)) void pt_sweep_ker
     // waves per trajectory the column tiles of half w / BT
     double2* stw = st + tw * TS;
     const bool c3 = p.cmul3 != 0;
+    const bool cbig = p.colbig != 0;
     auto col = [&](const double2* __restrict__ Op) {
-        if (c3) col_apply_mfma3<N2, CHI, RS, WPT>(Op, stw, lane, half);
-        else col_apply_mfma<N2, CHI, RS, WPT>(Op, stw, lane, half);
+        if (c3) {
+            if constexpr (col_big_ok<N2, CHI, RS, WPT>()) {
+                if (cbig) { col_apply_mfma3_big<N2, CHI, RS, WPT>(Op, stw, lane, half); return; }
+            }
+            col_apply_mfma3<N2, CHI, RS, WPT>(Op, stw, lane, half);
+        } else {
+            col_apply_mfma<N2, CHI, RS, WPT>(Op, stw, lane, half);
+        }
     };
     int ev_cur = 0, ev_lim = 0;
     {

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--fuse-modes", default="1", help="PQD_FUSE values to cross with the ablations")
     ap.add_argument("--config", default=None, help="a scripts/bench_configs.py config instead of the bench workload")
     ap.add_argument("--scan", type=int, default=None, help="with --config: override its scan points")
+    ap.add_argument("--env", default="", help="';'-separated environment variants ('A=1 B=0;A=0') crossed with the rest")
     args = ap.parse_args()
     import bench
     from pyaceqd_amd import engine
@@ -40,13 +41,20 @@ def main():
     else:
         sysd, grid, pt, rho0, ops, tr = bench.build_workload(args.traj, args.n_tau, args.chi)
     plans = {}
-    for fm in [int(x) for x in args.fuse_modes.split(",")]:
-        for pm in [int(x) for x in args.pt_modes.split(",")]:
-            for ab in [int(x) for x in args.variants.split(",")]:
-                os.environ["PQD_ABLATE"] = str(ab)
-                os.environ["PQD_PT_MODE"] = str(pm)
-                os.environ["PQD_FUSE"] = str(fm)
-                plans[f"fuse{fm}/pt{pm}/ab{ab}"] = engine.Plan(sysd, grid, rho0, ops, tr, pt=pt)
+    envs = [e.strip() for e in args.env.split(";")] if args.env else [""]
+    for ev in envs:
+        kv = dict(x.split("=", 1) for x in ev.split()) if ev else {}
+        for fm in [int(x) for x in args.fuse_modes.split(",")]:
+            for pm in [int(x) for x in args.pt_modes.split(",")]:
+                for ab in [int(x) for x in args.variants.split(",")]:
+                    os.environ["PQD_ABLATE"] = str(ab)
+                    os.environ["PQD_PT_MODE"] = str(pm)
+                    os.environ["PQD_FUSE"] = str(fm)
+                    os.environ.update(kv)
+                    tag = (ev.replace(" ", ",") + "/") if ev else ""
+                    plans[f"{tag}fuse{fm}/pt{pm}/ab{ab}"] = engine.Plan(sysd, grid, rho0, ops, tr, pt=pt)
+                    for k in kv:
+                        os.environ.pop(k, None)
     for k in ("PQD_ABLATE", "PQD_PT_MODE", "PQD_FUSE"):
         os.environ.pop(k, None)
     res = {v: [] for v in plans}
