@@ -206,6 +206,231 @@ __global__ __launch_bounds__(256) void free_prop_kernel(FreePropParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Large N2 (25, 36: the six-level and five-level systems) on the FP64 matrix cores. The same algorithm and degree
+// choice as free_prop_kernel, with every N2 x N2 complex product C = A B done as 4 x 4 blocks on
+// v_mfma_f64_4x4x4_4b (N2 = 36 is 9 x 9 blocks exactly; 25 is padded to 7 x 7): one instruction computes four
+// blocks D[blk] += A[blk] B[blk] (lane l = 16 k + 4 blk + x holds A[blk][x][k], B[blk][k][x], D[blk][l >> 4][x]),
+// so the 81 output blocks are 21 instruction slots of four, dealt to the four waves, each accumulating its slots over
+// the 9 k-blocks with 3 real products per complex product (3M). Operands stay in LDS with rows padded to an odd
+// stride; the result of a product stays in registers until the step that consumes it (Horner: P = A P / m + I,
+// squarings: P = P P, sub-steps: Acc = P Acc) writes it back after a barrier. The general kernel's 3 x 3 LDS blocks
+// ran the C5 scan's 132 k six-level propagators in 26.5 ms (≈30 TF/s).
+template <int N2>
+struct FPM {
+    static constexpr int NB = (N2 + 3) / 4;          // 4 x 4 blocks per dimension
+    static constexpr int NP = 4 * NB;                // padded dimension
+    static constexpr int LS = NP + 1;                // LDS row stride (complex)
+    static constexpr int NSLOT = NB * NB;            // output blocks
+    static constexpr int NG = (NSLOT + 3) / 4;       // instruction groups
+    static constexpr int GPW = (NG + 3) / 4;         // groups per wave (4 waves)
+    static constexpr size_t MAT = (size_t)NP * LS;   // complex elements per LDS matrix
+};
+
+// this lane's share of C = A B (A, B in LDS, padded, row stride LS): R[q] = element (row, col) of slot group
+// g = wave + 4 q, in the D-layout (row = 4 I + (l >> 4), col = 4 J + (l & 3)); rows/cols of dummy slots are not stored
+template <int N2>
+__device__ __forceinline__ void fpm_product(const double2* A, const double2* B, double2 (&R)[FPM<N2>::GPW], int wave,
+                                            int lane) {
+    using F = FPM<N2>;
+    const int k = lane >> 4, blk = (lane >> 2) & 3, x = lane & 3;
+    double p1[F::GPW], p2[F::GPW], p3[F::GPW];
+    int arow[F::GPW], bcol[F::GPW];
+#pragma unroll
+    for (int q = 0; q < F::GPW; ++q) {
+        p1[q] = 0.0; p2[q] = 0.0; p3[q] = 0.0;
+        int s = 4 * (wave + 4 * q) + blk;
+        s = s < F::NSLOT ? s : F::NSLOT - 1;   // dummy slots recompute the last block (not stored)
+        const int I = s / F::NB, J = s - (s / F::NB) * F::NB;
+        arow[q] = (4 * I + x) * F::LS + k;      // A[4 I + x][4 K + k]
+        bcol[q] = k * F::LS + 4 * J + x;        // B[4 K + k][4 J + x]
+    }
+#pragma unroll 3
+    for (int K = 0; K < F::NB; ++K) {
+#pragma unroll
+        for (int q = 0; q < F::GPW; ++q) {
+            if (wave + 4 * q >= F::NG) break;   // wave-uniform
+            const double2 a = A[arow[q] + 4 * K];
+            const double2 b = B[bcol[q] + 4 * K * F::LS];
+            p1[q] = __builtin_amdgcn_mfma_f64_4x4x4f64(a.x, b.x, p1[q], 0, 0, 0);
+            p2[q] = __builtin_amdgcn_mfma_f64_4x4x4f64(a.y, b.y, p2[q], 0, 0, 0);
+            p3[q] = __builtin_amdgcn_mfma_f64_4x4x4f64(a.x + a.y, b.x + b.y, p3[q], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < F::GPW; ++q) R[q] = make_double2(p1[q] - p2[q], p3[q] - p1[q] - p2[q]);
+}
+
+// the D-layout element of slot group q of this lane: its LDS index, or -1 (dummy slot, or padding beyond N2)
+template <int N2>
+__device__ __forceinline__ int fpm_index(int q, int wave, int lane, int& row, int& col) {
+    using F = FPM<N2>;
+    const int s = 4 * (wave + 4 * q) + ((lane >> 2) & 3);
+    if (wave + 4 * q >= F::NG || s >= F::NSLOT) return -1;
+    const int I = s / F::NB, J = s - (s / F::NB) * F::NB;
+    row = 4 * I + (lane >> 4);
+    col = 4 * J + (lane & 3);
+    return (row < N2 && col < N2) ? row * F::LS + col : -1;
+}
+
+template <int N2>
+__global__ __launch_bounds__(256) void free_prop_mfma_kernel(FreePropParams p) {
+    using F = FPM<N2>;
+    extern __shared__ __attribute__((aligned(16))) double2 smem[];
+    double2* A = smem;
+    double2* P = A + F::MAT;
+    double2* Acc = P + F::MAT;   // n_sub > 1 only
+    __shared__ double colsum[N2];
+    __shared__ int s_sh, s_deg;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // padding rows / columns stay zero for the whole launch (every product reads them, none writes them)
+    const int nmat = (p.n_sub > 1) ? 3 : 2;
+    for (int e = tid; e < (int)(nmat * F::MAT); e += 256) smem[e] = c_zero();
+    __syncthreads();
+    const long long nblk = p.idle_pass ? (long long)p.n_sys : (long long)p.n_sys * 2 * p.n_steps;
+    for (long long blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        const int si = p.idle_pass ? (int)blk : (int)(blk / (2 * p.n_steps));
+        const int m = p.idle_pass ? 0 : (int)(blk - (long long)si * 2 * p.n_steps);
+        const int n = m >> 1, h = m & 1;
+        const FreePropSys sy = p.systems[si];
+        const int nsub = p.n_sub > 0 ? p.n_sub : 1;
+        const double w = 0.5 * p.dt / nsub;
+        double2* out = p.idle_pass ? p.Midle + (size_t)si * N2 * N2 : p.M + ((size_t)si * 2 * p.n_steps + m) * N2 * N2;
+        if (!p.idle_pass && p.win) {
+            const int2 wn = p.win[si];
+            if (m < wn.x || m > wn.y) continue;
+        }
+        if (!p.idle_pass && p.Midle && idle_half_step(sy, p.ta + n * p.dt + h * 0.5 * p.dt, w, nsub)) {
+            const double2* src = p.Midle + (size_t)si * N2 * N2;
+            for (int e = tid; e < N2 * N2; e += 256) out[e] = src[e];
+            continue;
+        }
+        double2 R[F::GPW];
+        for (int j = 0; j < nsub; ++j) {
+            const double t = p.ta + n * p.dt + h * 0.5 * p.dt + (j + 0.5) * w;
+            double2 f[4], fc[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                if (c < sy.n_chan) {
+                    f[c] = p.idle_pass ? c_zero() : sample_ch(sy, c, t);
+                    fc[c] = c_conj(f[c]);
+                }
+            }
+            for (int e = tid; e < N2 * N2; e += 256) {
+                double2 v = sy.L0[e];
+                for (int c = 0; c < sy.n_chan; ++c) {
+                    c_fma(v, f[c], sy.S[(size_t)c * N2 * N2 + e]);
+                    c_fma(v, fc[c], sy.T[(size_t)c * N2 * N2 + e]);
+                }
+                const int i = e / N2, jj = e - i * N2;
+                A[i * F::LS + jj] = c_scale(v, w);
+            }
+            __syncthreads();
+            if (tid < N2) {
+                double s = 0.0;
+                for (int r = 0; r < N2; ++r) { const double2 a = A[r * F::LS + tid]; s += hypot(a.x, a.y); }
+                colsum[tid] = s;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                double norm = 0.0;
+                for (int c = 0; c < N2; ++c) norm = colsum[c] > norm ? colsum[c] : norm;
+                int e2 = 0;
+                frexp(norm / 0.5, &e2);
+                const int s = e2 > 0 ? e2 : 0;
+                const double theta = ldexp(norm, -s);
+                double rem = 0.5 * theta * theta;
+                int deg = 1;
+                while (deg < 18 && rem * 1.7 > 1.4e-17) { ++deg; rem *= theta / (deg + 1); }
+                s_sh = s;
+                s_deg = deg;
+            }
+            __syncthreads();
+            const int s = s_sh, deg = s_deg;
+            const double scale = ldexp(1.0, -s);
+            for (int e = tid; e < N2 * N2; e += 256) {
+                const int i = e / N2, jj = e - i * N2;
+                const double2 a = c_scale(A[i * F::LS + jj], scale);
+                A[i * F::LS + jj] = a;
+                double2 pv = make_double2(a.x / (double)deg, a.y / (double)deg);
+                if (i == jj) pv.x += 1.0;
+                P[i * F::LS + jj] = pv;
+            }
+            __syncthreads();
+            // Horner: P <- A P / mm + I
+            for (int mm = deg - 1; mm >= 1; --mm) {
+                fpm_product<N2>(A, P, R, wave, lane);
+                __syncthreads();
+#pragma unroll
+                for (int q = 0; q < F::GPW; ++q) {
+                    int r, c;
+                    const int ix = fpm_index<N2>(q, wave, lane, r, c);
+                    if (ix >= 0) {
+                        double2 pv = make_double2(R[q].x / (double)mm, R[q].y / (double)mm);
+                        if (r == c) pv.x += 1.0;
+                        P[ix] = pv;
+                    }
+                }
+                __syncthreads();
+            }
+            for (int qq = 0; qq < s; ++qq) {  // squarings
+                fpm_product<N2>(P, P, R, wave, lane);
+                __syncthreads();
+#pragma unroll
+                for (int q = 0; q < F::GPW; ++q) {
+                    int r, c;
+                    const int ix = fpm_index<N2>(q, wave, lane, r, c);
+                    if (ix >= 0) P[ix] = R[q];
+                }
+                __syncthreads();
+            }
+            if (nsub > 1) {
+                if (j == 0) {
+                    for (int e = tid; e < N2 * N2; e += 256) {
+                        const int i = e / N2, jj = e - i * N2;
+                        Acc[i * F::LS + jj] = P[i * F::LS + jj];
+                    }
+                } else {
+                    fpm_product<N2>(P, Acc, R, wave, lane);
+                    __syncthreads();
+#pragma unroll
+                    for (int q = 0; q < F::GPW; ++q) {
+                        int r, c;
+                        const int ix = fpm_index<N2>(q, wave, lane, r, c);
+                        if (ix >= 0) Acc[ix] = R[q];
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        const double2* res = (nsub == 1) ? P : Acc;
+        for (int e = tid; e < N2 * N2; e += 256) {
+            const int i = e / N2, jj = e - i * N2;
+            out[e] = res[i * F::LS + jj];
+        }
+        __syncthreads();
+    }
+}
+
+template <int N2>
+hipError_t launch_fpm(const FreePropParams& p, hipStream_t s) {
+    using F = FPM<N2>;
+    const size_t lds = (p.n_sub > 1 ? 3 : 2) * F::MAT * sizeof(double2);
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)free_prop_mfma_kernel<N2>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)(3 * F::MAT * sizeof(double2)));
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    const long long nblk = p.idle_pass ? (long long)p.n_sys : 2LL * p.n_steps * p.n_sys;
+    if (nblk <= 0) return hipSuccess;
+    hipLaunchKernelGGL(free_prop_mfma_kernel<N2>, dim3((unsigned)std::min<long long>(nblk, FP_MAX_BLOCKS)), dim3(256),
+                       lds, s, p);
+    return hipGetLastError();
+}
+
 // N2 = 4 (two-level system): a 4 x 4 matrix is 16 lanes, so a wave carries 4 matrices
 // and a 256-thread workgroup 16 — the general kernel would give each one a whole workgroup with 16 of
 // its 256 threads busy and a barrier per matmul. Lane (matrix, i, j) holds element (i, j) of A, P and
@@ -422,6 +647,60 @@ __global__ __launch_bounds__(256) void fuse_steps_kernel(FuseParams p) {
     }
 }
 
+// N2 = 25, 36: F(m) = M_a(m) M_b(m-1) as one matrix-core product (fpm_product) on the two operators staged in LDS;
+// W(m) = ovec . M_b(m-1) from the staged M_b. Same skips as fuse_steps_kernel.
+template <int N2>
+__global__ __launch_bounds__(256) void fuse_steps_mfma_kernel(FuseParams p) {
+    using F = FPM<N2>;
+    extern __shared__ __attribute__((aligned(16))) double2 smem[];
+    double2* Sa = smem;
+    double2* Sb = Sa + F::MAT;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int e = tid; e < (int)(2 * F::MAT); e += 256) smem[e] = c_zero();
+    __syncthreads();
+    const long long nblk = (long long)p.n_sys * p.n_steps;
+    for (long long blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        const int si = (int)(blk / p.n_steps), m = (int)(blk - (long long)si * p.n_steps) + 1;  // m = 1..n_steps
+        int2 wn = make_int2(INT_MIN, INT_MAX);
+        if (p.win) wn = p.win[si];
+        const bool out_b = 2 * m - 1 < wn.x || 2 * m - 1 > wn.y, out_a = 2 * m < wn.x || 2 * m > wn.y;
+        if (out_b && out_a) continue;
+        const double2* Mb = out_b ? p.Midle + (size_t)si * N2 * N2
+                                  : p.M + ((size_t)si * 2 * p.n_steps + 2 * (m - 1) + 1) * N2 * N2;
+        const bool hasF = m < p.n_steps;
+        const double2* Ma = (!hasF) ? Mb
+                          : out_a ? p.Midle + (size_t)si * N2 * N2 : p.M + ((size_t)si * 2 * p.n_steps + 2 * m) * N2 * N2;
+        for (int e = tid; e < N2 * N2; e += 256) {
+            const int i = e / N2, j = e - i * N2;
+            Sb[i * F::LS + j] = Mb[e];
+            if (hasF) Sa[i * F::LS + j] = Ma[e];
+        }
+        __syncthreads();
+        if (hasF) {
+            double2 R[F::GPW];
+            fpm_product<N2>(Sa, Sb, R, wave, lane);
+            double2* Fo = p.F + ((size_t)si * p.n_steps + m) * N2 * N2;
+#pragma unroll
+            for (int q = 0; q < F::GPW; ++q) {
+                int r, c;
+                if (fpm_index<N2>(q, wave, lane, r, c) >= 0) Fo[r * N2 + c] = R[q];
+            }
+        }
+        if (!out_b) {
+            double2* W = p.W + ((size_t)si * (p.n_steps + 1) + m) * p.n_out * N2;
+            for (int e = tid; e < p.n_out * N2; e += 256) {
+                const int k = e / N2, a = e - (e / N2) * N2;
+                double2 acc = c_zero();
+#pragma unroll 4
+                for (int b = 0; b < N2; ++b) c_fma(acc, p.ovec[k * N2 + b], Sb[b * F::LS + a]);
+                W[e] = acc;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // small N2: one thread per output element — F(m) entries, then W(m) entries — instead of a 256-thread workgroup per
 // step with N2^2 + n_out N2 of its threads busy (N2 = 4: 24 of 256). A workgroup takes FS_CHUNK steps of one system,
 // clipped to the steps whose F or W is stored (the pulse window) with one window load
@@ -512,6 +791,13 @@ hipError_t launch_fs(const FuseParams& p, hipStream_t s) {
                            0, s, p);
         return hipGetLastError();
     }
+    if constexpr (N2 >= 25) {
+        if (p.mfma) {
+            hipLaunchKernelGGL(fuse_steps_mfma_kernel<N2>, dim3((unsigned)std::min<long long>(nblk, FP_MAX_BLOCKS)),
+                               dim3(256), 2 * FPM<N2>::MAT * sizeof(double2), s, p);
+            return hipGetLastError();
+        }
+    }
     hipLaunchKernelGGL(fuse_steps_kernel<N2>, dim3((unsigned)std::min<long long>(nblk, FP_MAX_BLOCKS)), dim3(256), 0,
                        s, p);
     return hipGetLastError();
@@ -545,8 +831,8 @@ static hipError_t launch_free_prop_pass(int N2, const FreePropParams& p, hipStre
         case 4: return launch_fp<4>(p, s);
         case 9: return launch_fp<9>(p, s);
         case 16: return launch_fp<16>(p, s);
-        case 25: return launch_fp<25>(p, s);
-        case 36: return launch_fp<36>(p, s);
+        case 25: return p.mfma ? launch_fpm<25>(p, s) : launch_fp<25>(p, s);
+        case 36: return p.mfma ? launch_fpm<36>(p, s) : launch_fp<36>(p, s);
         default: return hipErrorInvalidValue;
     }
 }

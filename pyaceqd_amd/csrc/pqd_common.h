@@ -53,6 +53,7 @@ struct FreePropParams {
     int2* win;               // n_sys pulse windows (lo, hi): every half step h < lo or h > hi is idle and is NOT stored
                              //   (readers take Midle, see fw_M); NULL: every half step stored (copies of Midle)
     int chunk;               // free_prop4_kernel: half steps per workgroup (set by its launcher)
+    int mfma;                // N2 = 25, 36: products on the matrix cores (free_prop_mfma_kernel; PQD_FPM=0: LDS kernel)
 };
 
 struct SweepParams {
@@ -188,6 +189,7 @@ struct FuseParams {          // F(m) = M_a(m) M_b(m-1) (1 <= m < n_steps), W(m) 
     const double2* Midle;    // with win: the idle pass writes Fidle = Midle Midle and Widle = ovec . Midle per system
     double2* Fidle;
     double2* Widle;
+    int mfma;                // N2 = 25, 36: F(m) on the matrix cores (fuse_steps_mfma_kernel; follows PQD_FPM)
 };
 
 hipError_t launch_free_prop(int N2, const FreePropParams& p, hipStream_t s);

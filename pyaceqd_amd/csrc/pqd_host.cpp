@@ -434,6 +434,7 @@ int pqd_free_propagators(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* gr
     fp.systems = tab.p; fp.n_sys = 1;
     fp.ta = grid->ta; fp.dt = grid->dt; fp.n_steps = grid->n_steps; fp.n_sub = grid->n_sub; fp.M = M.p;
     { const char* f4 = getenv("PQD_FP4"); fp.packed4 = (f4 && atoi(f4) == 0) ? 0 : 1; }
+    { const char* fm = getenv("PQD_FPM"); fp.mfma = (fm && atoi(fm) == 0) ? 0 : 1; }
     if (const char* ie = getenv("PQD_IDLE"); !(ie && atoi(ie) == 0)) {
         HIPCHK(Mi.alloc((size_t)N2 * N2));
         fp.Midle = Mi.p;
@@ -997,6 +998,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     // it (tests provoke the batched fallback with 0)
     { const char* sl = getenv("PQD_SPLIT_SPIN"); sp.spin_limit = sl ? (unsigned)strtoul(sl, nullptr, 10) : (1u << 22); }
     { const char* f4 = getenv("PQD_FP4"); P->fp.packed4 = (f4 && atoi(f4) == 0) ? 0 : 1; }
+    { const char* fm = getenv("PQD_FPM"); P->fp.mfma = (fm && atoi(fm) == 0) ? 0 : 1; }
     HIPCHK(P->flags.alloc(4));
     HIPCHK(hipMemsetAsync(P->flags.p, 0, 4 * sizeof(unsigned), s));
     sp.flags = P->flags.p;
@@ -1021,6 +1023,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
         HIPCHK(P->F.alloc((size_t)n_sys * ns * m2));
         HIPCHK(P->W.alloc((size_t)n_sys * (ns + 1) * n_out * N2));
         P->fu = FuseParams{P->M.p, P->F.p, P->W.p, P->ovec.p, n_sys, ns, n_out};
+        P->fu.mfma = P->fp.mfma;
         if (P->win.p) {
             HIPCHK(P->Fidle.alloc((size_t)n_sys * m2));
             HIPCHK(P->Widle.alloc((size_t)n_sys * n_out * N2));
