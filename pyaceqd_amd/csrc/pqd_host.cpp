@@ -434,7 +434,7 @@ int pqd_free_propagators(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* gr
     fp.systems = tab.p; fp.n_sys = 1;
     fp.ta = grid->ta; fp.dt = grid->dt; fp.n_steps = grid->n_steps; fp.n_sub = grid->n_sub; fp.M = M.p;
     { const char* f4 = getenv("PQD_FP4"); fp.packed4 = (f4 && atoi(f4) == 0) ? 0 : 1; }
-    { const char* fm = getenv("PQD_FPM"); fp.mfma = (fm && atoi(fm) == 0) ? 0 : 1; }
+    { const char* fm = getenv("PQD_FPM"); fp.mfma = fm ? atoi(fm) : 1; }
     if (const char* ie = getenv("PQD_IDLE"); !(ie && atoi(ie) == 0)) {
         HIPCHK(Mi.alloc((size_t)N2 * N2));
         fp.Midle = Mi.p;
@@ -466,12 +466,39 @@ static std::vector<int4> pt_row_units(const std::vector<int>& gmap, int NW, int 
     std::stable_sort(units.begin(), units.end(), [&](const int4& x, const int4& y) { return cost(x) > cost(y); });
     std::vector<std::vector<int4>> per(NW);
     std::vector<int> load(NW, 0);
+    // the PT phase lasts as long as the most-loaded wave: aim at T = ceil(rows / waves) rows per wave. Whole units go
+    // to the least-loaded wave they fit (largest first); a unit that fits nowhere is split into its rows,
+    // which then fill the waves' remaining capacity, rows of one slice kept together per wave (a split slice is read
+    // once more from L2 per extra wave). Six-level dictionary PT (9 slices x 4 rows, 8 waves): max 5 rows per wave
+    // instead of 8 (one wave held two 4-row units). Least-loaded first, so the two waves of a SIMD (w, w + NW / 2)
+    // also stay balanced: their MFMAs share its matrix pipe
+    int T = (N2 + NW - 1) / NW;
+    if (const char* e = getenv("PQD_UNITBAL"); e && atoi(e) == 0) T = 1 << 20;  // A/B: whole units, least loaded
+    std::vector<int> pending;  // rows of split units, slice-ordered
     for (const int4& e : units) {
-        int w = 0;
+        int w = -1;
+        for (int k = 0; k < NW; ++k)
+            if (load[k] + cost(e) <= T && (w < 0 || load[k] < load[w])) w = k;
+        if (w >= 0) {
+            per[w].push_back(e);
+            load[w] += cost(e);
+            continue;
+        }
+        const int rows[4] = {e.y, e.z, e.w >= 0 ? (e.w & 0xFFFF) : -1, e.w >= 0 ? (e.w >> 16) : -1};
+        for (int r : rows)
+            if (r >= 0 && r != 0x7FFF) pending.push_back(r);
+    }
+    for (size_t i = 0; i < pending.size();) {
+        int w = 0;  // the least-loaded wave takes as many rows of this slice as fit (at most rmax)
         for (int k = 1; k < NW; ++k)
             if (load[k] < load[w]) w = k;
-        per[w].push_back(e);
-        load[w] += cost(e);
+        const int room = std::max(1, std::min(rmax, T - load[w]));
+        int rows[4] = {-1, -1, -1, -1}, cnt = 0;
+        const int g = gmap[pending[i]];
+        while (i < pending.size() && cnt < room && gmap[pending[i]] == g) rows[cnt++] = pending[i++];
+        const int wv = cnt > 2 ? (rows[2] | ((cnt > 3 ? rows[3] : 0x7FFF) << 16)) : -1;
+        per[w].push_back(make_int4(g, rows[0], rows[1], wv));
+        load[w] += cnt;
     }
     size_t umax = 1;
     for (auto& v : per) umax = std::max(umax, v.size() + 1);
@@ -998,7 +1025,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     // it (tests provoke the batched fallback with 0)
     { const char* sl = getenv("PQD_SPLIT_SPIN"); sp.spin_limit = sl ? (unsigned)strtoul(sl, nullptr, 10) : (1u << 22); }
     { const char* f4 = getenv("PQD_FP4"); P->fp.packed4 = (f4 && atoi(f4) == 0) ? 0 : 1; }
-    { const char* fm = getenv("PQD_FPM"); P->fp.mfma = (fm && atoi(fm) == 0) ? 0 : 1; }
+    { const char* fm = getenv("PQD_FPM"); P->fp.mfma = fm ? atoi(fm) : 1; }
     HIPCHK(P->flags.alloc(4));
     HIPCHK(hipMemsetAsync(P->flags.p, 0, 4 * sizeof(unsigned), s));
     sp.flags = P->flags.p;

@@ -216,7 +216,7 @@ def run_c5dm(steps, n_e0=2, bxs=(0.0, 1.0, 2.0, 4.0), tend=400.0):
     n_tau = int(round(tend / 0.1))
     executed = 3 * sum(int(np.sum(n_tau + 1 - np.minimum(n_tau, (np.asarray(x.t1) / 0.1).astype(int))))
                        for x in insts)
-    return {"config": "c5dm", "model": "sixls", "points": len(insts), "e0": n_e0, "bx": list(bxs), "tend": tend,
+    return {"config": "c5dm" if len(insts) == 8 else f"c5dm{len(insts)}", "model": "sixls", "points": len(insts), "e0": n_e0, "bx": list(bxs), "tend": tend,
             "chi": 64, "N": 6, "n_out": "6/8/6", "launches": 3, "n_traj": n_traj,
             "output_traj_steps": executed, "wall_s_per_scan": el, "points_per_s": len(insts) / el,
             "output_traj_steps_per_s": executed / el, "concurrence": [float(c) for c in conc]}
@@ -228,7 +228,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     args = ap.parse_args()
     for name in args.configs.split(","):
-        special = {"c5dm": run_c5dm, "c4reuse": run_c4reuse}
+        # c5dm32: one rank's share of SURVEY §8d C5 (256 points = 64 e0 x 4 bx over 8 GPUs): 8 e0 x 4 bx
+        special = {"c5dm": run_c5dm, "c4reuse": run_c4reuse, "c5dm32": lambda st: run_c5dm(st, n_e0=8)}
         print(json.dumps(special[name](args.steps) if name in special else run(name, args.steps)), flush=True)
 
 
