@@ -154,6 +154,17 @@ int pqd_propagate_table(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems, 
                         int32_t n_out, const pqd_c128* out_ops, const pqd_traj* traj, pqd_c128* table,
                         int64_t table_len);
 
+/* pqd_propagate_table's run reduced on the device to trapezoid integrals over each trajectory's output window, in
+ * place of the tables: with y_k(s) = output k at window step s (s = 0 .. L_t - 1) and a uniform spacing dx,
+ *   res[t * n_pairs + q] = dx * (y_{k_head[q]}(0) / 2 + sum_{s=1}^{L_t-2} y_{k_tail[q]}(s) + y_{k_tail[q]}(L_t - 1) / 2)
+ * (0 when L_t < 2). This is the tau integral of G2_reuse (pol_entanglement/G2.py:484-505: tau = 0 from
+ * <op1 op2 op3 op4> at t1, tau > 0 from <op2 op3>, np.trapz over t2) for every t1 trajectory at once; only
+ * n_traj * n_pairs values leave the device. pqd_plan_trapz: the same reduction of an executed plan's outputs. */
+int pqd_propagate_trapz(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems, const int32_t* traj_sys,
+                        const pqd_grid* grid, const pqd_pt* pt, const int32_t* sched, const pqd_c128* rho0,
+                        int32_t n_out, const pqd_c128* out_ops, const pqd_traj* traj, int32_t n_pairs,
+                        const int32_t* k_head, const int32_t* k_tail, double dx, pqd_c128* res);
+
 /* device-resident plan for repeated execution (bench, scans): same arguments as pqd_propagate(_multi). */
 int pqd_plan_create(pqd_ctx* ctx, const pqd_system* sys, const pqd_grid* grid, const pqd_pt* pt,
                     const int32_t* sched, const pqd_c128* rho0, int32_t n_out, const pqd_c128* out_ops,
@@ -180,6 +191,8 @@ int pqd_plan_copy_output(pqd_plan* plan, void* dst, int64_t out_len);
 /* the plan's ACE-table length (complex values, layout of pqd_propagate_table) and pqd_plan_synchronize + the tables */
 int pqd_plan_table_len(const pqd_plan* plan, int64_t* table_len);
 int pqd_plan_download_table(pqd_plan* plan, pqd_c128* table, int64_t table_len);
+int pqd_plan_trapz(pqd_plan* plan, int32_t n_pairs, const int32_t* k_head, const int32_t* k_tail, double dx,
+                   pqd_c128* res);
 #define PQD_PATH_NOPT 0     /* no PT: one wave per trajectory */
 #define PQD_PATH_BATCHED 1  /* lock-step PT sweep, bt trajectories per workgroup */
 #define PQD_PATH_SPLIT 2    /* one trajectory over N^2 workgroups (latency path) */

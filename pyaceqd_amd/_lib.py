@@ -78,6 +78,9 @@ _SIGS = {
                              P_I32, P_C128, C.c_int32, P_C128, C.POINTER(pqd_traj), P_C128, C.c_int64], C.c_int),
     "pqd_propagate_table": ([C.c_void_p, C.c_int32, C.POINTER(pqd_system), P_I32, C.POINTER(pqd_grid), C.c_void_p,
                              P_I32, P_C128, C.c_int32, P_C128, C.POINTER(pqd_traj), P_C128, C.c_int64], C.c_int),
+    "pqd_propagate_trapz": ([C.c_void_p, C.c_int32, C.POINTER(pqd_system), P_I32, C.POINTER(pqd_grid), C.c_void_p,
+                             P_I32, P_C128, C.c_int32, P_C128, C.POINTER(pqd_traj), C.c_int32, P_I32, P_I32,
+                             C.c_double, P_C128], C.c_int),
     "pqd_plan_create_multi": ([C.c_void_p, C.c_int32, C.POINTER(pqd_system), P_I32, C.POINTER(pqd_grid),
                                C.c_void_p, P_I32, P_C128, C.c_int32, P_C128, C.POINTER(pqd_traj), C.c_int64,
                                C.POINTER(C.c_void_p)], C.c_int),
@@ -90,6 +93,7 @@ _SIGS = {
     "pqd_plan_copy_output": ([C.c_void_p, C.c_void_p, C.c_int64], C.c_int),
     "pqd_plan_table_len": ([C.c_void_p, P_I64], C.c_int),
     "pqd_plan_download_table": ([C.c_void_p, P_C128, C.c_int64], C.c_int),
+    "pqd_plan_trapz": ([C.c_void_p, C.c_int32, P_I32, P_I32, C.c_double, P_C128], C.c_int),
     "pqd_plan_windows": ([C.c_void_p, P_I32], C.c_int),
     "pqd_plan_info": ([C.c_void_p, P_I32, P_I32, P_I32, P_I64], C.c_int),
     "pqd_plan_timing": ([C.c_void_p, P_F64, P_F64, P_I32, C.c_int32], C.c_int),

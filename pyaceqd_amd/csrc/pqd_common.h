@@ -201,6 +201,8 @@ hipError_t launch_table(const double2* out, const long long* woff, const int* wb
                         const long long* toff, int n_traj, int n_out, double t_start, double dt, double2* table,
                         hipStream_t s);
 hipError_t launch_fuse_steps(int N2, const FuseParams& p, hipStream_t s);
+hipError_t launch_trapz(const double2* out, const long long* woff, const int* wbeg, const int* wend, int n_traj,
+                        int n_out, int n_pairs, const int* kh, const int* kt, double dx, double2* res, hipStream_t s);
 // waves per trajectory in the PT sweep: a 4-trajectory workgroup (N2 > 16 or chi = 128) runs 8 waves, two per
 // trajectory (each owns half of the bond columns in the column phases), so every SIMD holds two waves
 // (N2 = 4 included: one wave per trajectory there, four waves per workgroup and two workgroups per CU, measured

@@ -1193,6 +1193,49 @@ int pqd_plan_download_table(pqd_plan* P, pqd_c128* table, int64_t table_len) {
     return rc;
 }
 
+int pqd_plan_trapz(pqd_plan* P, int32_t n_pairs, const int32_t* k_head, const int32_t* k_tail, double dx,
+                   pqd_c128* res) {
+    if (!P || (n_pairs > 0 && (!k_head || !k_tail || !res))) return fail(PQD_ERR_ARG, "NULL argument");
+    if (n_pairs < 0) return fail(PQD_ERR_ARG, "n_pairs %d < 0", n_pairs);
+    for (int q = 0; q < n_pairs; ++q)
+        if (k_head[q] < 0 || k_head[q] >= P->n_out || k_tail[q] < 0 || k_tail[q] >= P->n_out)
+            return fail(PQD_ERR_ARG, "pair %d: output (%d, %d) not in [0, %d)", q, k_head[q], k_tail[q], P->n_out);
+    int rc = pqd_plan_synchronize(P);
+    if (rc && rc != PQD_ERR_NUMERIC) return rc;
+    const size_t n = (size_t)P->n_traj * n_pairs;
+    if (n == 0) return rc;
+    hipStream_t s = P->ctx->stream;
+    DevBuf<int> kd;
+    DevBuf<double2> rd;
+    std::vector<int> k(2 * (size_t)n_pairs);
+    for (int q = 0; q < n_pairs; ++q) { k[q] = k_head[q]; k[n_pairs + q] = k_tail[q]; }
+    HIPCHK(kd.upload(k.data(), k.size(), s));
+    HIPCHK(rd.alloc(n));
+    HIPCHK(launch_trapz(P->out.p, P->woff.p, P->wbeg.p, P->wend.p, P->n_traj, P->n_out, n_pairs, kd.p, kd.p + n_pairs,
+                        dx, rd.p, s));
+    HIPCHK(hipMemcpyAsync(res, rd.p, n * sizeof(double2), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return rc;
+}
+
+int pqd_propagate_trapz(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems, const int32_t* traj_sys,
+                        const pqd_grid* grid, const pqd_pt* pt, const int32_t* sched, const pqd_c128* rho0,
+                        int32_t n_out, const pqd_c128* out_ops, const pqd_traj* tr, int32_t n_pairs,
+                        const int32_t* k_head, const int32_t* k_tail, double dx, pqd_c128* res) {
+    if (!tr) return fail(PQD_ERR_ARG, "NULL argument");
+    int64_t out_len = 0;
+    for (int t = 0; t < tr->n_traj; ++t)
+        out_len = std::max<int64_t>(out_len, tr->out_offset[t] + (int64_t)(tr->out_end[t] - tr->out_begin[t] + 1) * n_out);
+    pqd_plan* P = nullptr;
+    int rc = pqd_plan_create_multi(ctx, n_sys, systems, traj_sys, grid, pt, sched, rho0, n_out, out_ops, tr,
+                                   std::max<int64_t>(1, out_len), &P);
+    if (rc) return rc;
+    rc = pqd_plan_execute(P, 1);
+    if (!rc) rc = pqd_plan_trapz(P, n_pairs, k_head, k_tail, dx, res);
+    pqd_plan_destroy(P);
+    return rc;
+}
+
 int pqd_plan_copy_output(pqd_plan* P, void* dst, int64_t out_len) {
     if (!P || !dst) return fail(PQD_ERR_ARG, "NULL argument");
     if (out_len < P->out_len) return fail(PQD_ERR_ARG, "out_len %lld < plan out_len %lld", (long long)out_len, (long long)P->out_len);

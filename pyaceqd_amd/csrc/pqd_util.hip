@@ -35,7 +35,44 @@ __global__ __launch_bounds__(256) void table_kernel(const double2* __restrict__ 
     }
 }
 
+// trapezoid integrals over each trajectory's window (pqd_plan_trapz): one wave per (trajectory, pair), lanes over the
+// interior steps 1 .. L-2 of the tail output, a 64-lane tree sum; res = dx (y_head(0) / 2 + interior + y_tail(L-1) / 2)
+__global__ __launch_bounds__(256) void trapz_kernel(const double2* __restrict__ out, const long long* __restrict__ woff,
+                                                    const int* __restrict__ wbeg, const int* __restrict__ wend,
+                                                    int n_traj, int n_out, int n_pairs, const int* __restrict__ kh,
+                                                    const int* __restrict__ kt, double dx, double2* __restrict__ res) {
+    const int lane = threadIdx.x & 63;
+    const long long n_items = (long long)n_traj * n_pairs;
+    for (long long it = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); it < n_items; it += (long long)gridDim.x * 4) {
+        const int t = (int)(it / n_pairs), q = (int)(it - (long long)t * n_pairs);
+        const int L = wend[t] - wbeg[t] + 1;
+        const double2* o = out + woff[t];
+        const int a = kh[q], b = kt[q];
+        double2 acc = c_zero();
+        for (int i = 1 + lane; i < L - 1; i += 64) acc = c_add(acc, o[(size_t)i * n_out + b]);
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) acc = c_add(acc, c_shfl_xor(acc, m));
+        if (lane == 0) {
+            double2 v = c_zero();
+            if (L >= 2) {
+                const double2 h = o[a], e = o[(size_t)(L - 1) * n_out + b];
+                v = c_scale(make_double2(0.5 * h.x + acc.x + 0.5 * e.x, 0.5 * h.y + acc.y + 0.5 * e.y), dx);
+            }
+            res[it] = v;
+        }
+    }
+}
+
 }  // namespace
+
+hipError_t launch_trapz(const double2* out, const long long* woff, const int* wbeg, const int* wend, int n_traj,
+                        int n_out, int n_pairs, const int* kh, const int* kt, double dx, double2* res, hipStream_t s) {
+    const long long items = (long long)n_traj * n_pairs;
+    if (items <= 0) return hipSuccess;
+    hipLaunchKernelGGL(trapz_kernel, dim3((unsigned)std::min<long long>((items + 3) / 4, 1 << 16)), dim3(256), 0, s, out,
+                       woff, wbeg, wend, n_traj, n_out, n_pairs, kh, kt, dx, res);
+    return hipGetLastError();
+}
 
 hipError_t launch_table(const double2* out, const long long* woff, const int* wbeg, const int* wend,
                         const long long* toff, int n_traj, int n_out, double t_start, double dt, double2* table,

@@ -279,6 +279,30 @@ def tables_from_outputs(outs, traj: Trajectories, grid: Grid):
     return res
 
 
+def propagate_trapz(system, grid: Grid, rho0, out_ops: Sequence, traj: Trajectories, k_head, k_tail, dx,
+                    pt: Optional[ProcessTensor] = None, ctx=None):
+    """propagate() reduced on the device to trapezoid integrals over each trajectory's output window
+    (pqd_propagate_trapz): res[t, q] = dx (y_{k_head[q]}(0) / 2 + sum_{s=1}^{L-2} y_{k_tail[q]}(s) + y_{k_tail[q]}(L-1) / 2),
+    0 for windows shorter than 2 steps. The tau integrals of G2_reuse (pol_entanglement/G2.py:484-505) without
+    downloading the tables. Returns (n_traj, n_pairs) complex."""
+    ctx = ctx or _lib.context()
+    dim = _systems(system)[0].dim
+    kh = np.ascontiguousarray(k_head, dtype=np.int32)
+    kt = np.ascontiguousarray(k_tail, dtype=np.int32)
+    if kh.shape != kt.shape or kh.ndim != 1:
+        raise ValueError("k_head and k_tail must be 1-D of equal length")
+    res = np.zeros((max(1, traj.n_traj), max(1, len(kh))), dtype=np.complex128)
+    with ctx.lock:
+        keep, total = _prep(system, grid, rho0, out_ops, traj, pt, ctx)
+        k1, k2, r0, ops, sched, sc, gc, tc, tsys, n_sys = keep
+        pth = pt.handle(ctx, dim) if pt is not None else None
+        _lib.check(_lib.lib().pqd_propagate_trapz(ctx.handle, n_sys, sc, _lib.iptr(tsys), C.byref(gc), pth,
+                                                  _lib.iptr(sched), _lib.cptr(r0), len(out_ops), _lib.cptr(ops),
+                                                  C.byref(tc), len(kh), _lib.iptr(kh), _lib.iptr(kt), float(dx),
+                                                  _lib.cptr(res)))
+    return res[: traj.n_traj, : len(kh)]
+
+
 def propagate_table(system, grid: Grid, rho0, out_ops: Sequence, traj: Trajectories,
                     pt: Optional[ProcessTensor] = None, ctx=None):
     """propagate() returning ACE's output table per trajectory: (1 + n_out, window_len) arrays, row 0 = the step

@@ -10,7 +10,7 @@ from .. import constants
 hbar = constants.hbar
 temp_dir = constants.temp_dir
 
-_FWD = ("trajectories", "n_sub", "device", "rho0", "get_M_t", "pulse_sampling")
+_FWD = ("trajectories", "n_sub", "device", "rho0", "get_M_t", "pulse_sampling", "trapz")
 
 
 def biexciton_ops(delta_xy=0, shift_x=True, coupl_xy=0, delta_b=4, gamma_e=1/100, gamma_b=None, lindblad=False,

@@ -28,7 +28,8 @@ import numpy as np
 from ..constants import hbar
 from .. import constants
 from .. import opgrammar
-from ..engine import Grid, MTO, ProcessTensor, System, Trajectories, free_propagators, propagate, propagate_table, KIND
+from ..engine import Grid, MTO, ProcessTensor, System, Trajectories, free_propagators, propagate, propagate_table, \
+    propagate_trapz, KIND
 
 temp_dir = constants.temp_dir
 
@@ -177,7 +178,7 @@ def system_ace_stream(t_start, t_end, *pulses, dt=0.01, phonons=False, t_mem=20.
                       prepare_only=False, LO_params=None, dressedstates=False, rf_op=None, rf_file=None,
                       firstonly=False, J_to_file=None, J_file=None, factor_ah=None, use_infinite=False,
                       print_H=False, calc_dynmap=False, rho0=None, get_M_t=None, trajectories=None, n_sub=1,
-                      device=None, pulse_sampling="exact"):
+                      device=None, pulse_sampling="exact", trapz=None):
     """Propagate one trajectory (or a batch: `trajectories`) and return ACE's output table.
 
     Returns (1 + len(output_ops), n_t) complex, row 0 = time (general_system.py:104-110, 343).
@@ -361,6 +362,15 @@ def system_ace_stream(t_start, t_end, *pulses, dt=0.01, phonons=False, t_mem=20.
     multi = len(systems) > 1
     tr = Trajectories(np.array(begins), np.array(ends), mtos, system=np.array(traj_sys) if multi else None)
     from .. import _lib
+    if trapz is not None:
+        # (k_head, k_tail, dx): per-trajectory trapezoid integrals of output rows over the window, on the device
+        # (pqd_propagate_trapz), in place of the tables: (n_traj, n_pairs) complex
+        if not n_real:
+            raise ValueError("trapz needs output_ops")
+        k_head, k_tail, dx = trapz
+        res = propagate_trapz(systems if multi else system, grid, rho_init, out_mats, tr, k_head, k_tail, dx, pt=pt,
+                              ctx=_lib.context(device))
+        return res if trajectories is not None else res[0]
     if n_real:
         # ACE's output table per trajectory, assembled on the device (pqd_propagate_table): views, no host copies
         res = propagate_table(systems if multi else system, grid, rho_init, out_mats, tr, pt=pt,

@@ -429,6 +429,10 @@ def densitymatrix_reuse_scan(instances, model_kwargs=None, return_rho=False):
         diff = _options_differ(first.options, x.options)
         if diff:
             raise ValueError(f"the points of a scan must share their options; they differ in {sorted(diff)}")
+    # the tau integrals on the device (pqd_propagate_trapz: only n_traj x n_pairs values leave it) unless
+    # PQD_SCAN_TRAPZ=0 (tables downloaded, integrals on the host as calc_densitymatrix_reuse does)
+    on_device = os.environ.get("PQD_SCAN_TRAPZ", "1") != "0"
+
     def variant(v):
         specs, counts, outs, n_tau = [], [], None, None
         for x, k in zip(insts, kw):
@@ -441,10 +445,19 @@ def densitymatrix_reuse_scan(instances, model_kwargs=None, return_rho=False):
             counts.append(len(sp))
         opts = dict(first.options)
         opts["output_ops"] = outs
+        n_pairs = len(first._reuse_variants()[v][1])
+        if on_device:
+            # G2_reuse's trapezoid over t2 = linspace(0, tend, n_tau + 1) (reference :484-505): head <op1 op2 op3 op4>
+            # at t1 (output n_pairs + j), tail <op2 op3> after it (output j); every window is [int(t1/dt), n_tau]
+            opts["trapz"] = (list(range(n_pairs, 2 * n_pairs)), list(range(n_pairs)), first.tend / n_tau)
         res = first.system(0, first.tend, trajectories=specs, **opts)
         got, o = [], 0
         for i, x in enumerate(insts):
-            got.append(x._reuse_integrals(res[o: o + counts[i]], len(x._reuse_variants()[v][1]), n_tau))
+            if on_device:
+                g = np.ascontiguousarray(res[o: o + counts[i]].T)
+                got.append((x.t1, g, _trapz(g, x.t1, axis=1)))
+            else:
+                got.append(x._reuse_integrals(res[o: o + counts[i]], n_pairs, n_tau))
             o += counts[i]
         return got
 

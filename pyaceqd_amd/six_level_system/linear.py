@@ -21,7 +21,7 @@ g_ez = -0.8   # out of plane electron g factor
 g_hx = -0.35  # in plane hole g factor
 g_hz = -2.2   # out of plane hole g factor
 
-_FWD = ("trajectories", "n_sub", "device", "rho0", "get_M_t", "calc_dynmap", "pulse_sampling")
+_FWD = ("trajectories", "n_sub", "device", "rho0", "get_M_t", "calc_dynmap", "pulse_sampling", "trapz")
 
 
 def energies_linear(d0=0.25, d1=0.12, d2=0.05, delta_B=4, delta_E=0.0):

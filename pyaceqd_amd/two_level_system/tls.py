@@ -11,7 +11,7 @@ from .. import constants
 hbar = constants.hbar
 temp_dir = constants.temp_dir
 
-_FWD = ("trajectories", "n_sub", "device", "pulse_sampling")
+_FWD = ("trajectories", "n_sub", "device", "pulse_sampling", "trapz")
 
 
 def tls(t_start, t_end, *pulses, dt=0.1, gamma_e=1/100, phonons=False, t_mem=6.4, ae=5.0, temperature=4,

@@ -196,6 +196,37 @@ def test_output_tables_match_flat_outputs(chi):
         assert np.array_equal(g, w)
 
 
+@pytest.mark.parametrize("chi", [1, 16, 32])
+def test_output_trapz_matches_host_integrals(chi):
+    """pqd_propagate_trapz / Plan-free device reduction (the G2_reuse tau integral, pol_entanglement/G2.py:484-505):
+    dx (y_head(0) / 2 + interior of y_tail + y_tail(L-1) / 2) per trajectory and pair, vs the same sum over the flat
+    outputs on the host; windows of 1 (-> 0), 2 and many steps, ragged, two systems; out-of-range pairs refused"""
+    N = 2 if chi == 32 else 4
+    s1, grid = H.random_system(N, n_steps=40, seed=3)
+    s2, _ = H.random_system(N, n_steps=40, seed=4)
+    pt = ptmod.random_pt(N, chi, D=N * N, n_slices=41, seed=5, eps=0.1) if chi > 1 else None
+    tr = _traj(grid.n_steps, N, 21, seed=2)
+    b, e = tr.out_begin.copy(), tr.out_end.copy()
+    b[0], e[0] = 7, 7      # one step: no interval
+    b[1], e[1] = 3, 4      # two steps: head and last tail point only
+    tr = Trajectories(b, e, tr.mtos, system=np.arange(tr.n_traj) % 2)
+    ops = [H.ketbra(N, a, c) for a in range(N) for c in range(N)][:5]
+    rho0 = H.random_rho(N)
+    no = len(ops)
+    kh, kt, dx = [no - 2, no - 1, 0], [0, 1, 2], 0.25
+    got = engine.propagate_trapz([s1, s2], grid, rho0, ops, tr, kh, kt, dx, pt=pt)
+    flat = engine.propagate([s1, s2], grid, rho0, ops, tr, pt=pt)
+    assert got.shape == (tr.n_traj, 3)
+    for t, y in enumerate(flat):
+        for q in range(3):
+            L = y.shape[0]
+            want = 0.0 if L < 2 else dx * (0.5 * y[0, kh[q]] + y[1: L - 1, kt[q]].sum() + 0.5 * y[L - 1, kt[q]])
+            assert abs(got[t, q] - want) <= 1e-13 * max(1.0, abs(want))
+    assert np.all(got[0] == 0)
+    with pytest.raises(ValueError, match="not in"):
+        engine.propagate_trapz([s1, s2], grid, rho0, ops, tr, [no], [0], dx, pt=pt)
+
+
 def test_empty_batch_and_zero_steps():
     sysd, grid = H.random_system(2, n_steps=0, seed=0)
     tr = Trajectories(np.array([0]), np.array([0]))
