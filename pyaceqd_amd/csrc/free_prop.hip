@@ -830,7 +830,7 @@ static hipError_t launch_free_prop_pass(int N2, const FreePropParams& p, hipStre
     switch (N2) {
         case 4: return launch_fp<4>(p, s);
         case 9: return launch_fp<9>(p, s);
-        case 16: return launch_fp<16>(p, s);
+        case 16: return p.mfma ? launch_fpm<16>(p, s) : launch_fp<16>(p, s);
         case 25: return p.mfma ? launch_fpm<25>(p, s) : launch_fp<25>(p, s);
         case 36: return p.mfma ? launch_fpm<36>(p, s) : launch_fp<36>(p, s);
         default: return hipErrorInvalidValue;
