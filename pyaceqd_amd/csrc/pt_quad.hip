@@ -426,10 +426,6 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : (NCG =
     // n + 2 sit between the contraction's MFMAs (the compiler interleaves them within the block), and the closure
     // partial of the next step sits beside its column operator. Critical path per step: D -> C relayout, F(n) on the
     // matrix cores, exchange + barrier, A-operand reads, the contraction.
-    auto fast_ok = [&](int n) -> bool {
-        return n != next_act && n < q_hi && n < n_hi && fuse && NO <= 4 && !(p.ablate & 31) &&
-               !__ballot(traj >= 0 && (n < act || !fz || evn.x == n || evn.x == n + 1));
-    };
     // ring slot S (compile time): step n's operands; after use the slot fetches step n + 2 (no register moves,
     // so each fetch has two steps to arrive; see the loop below)
     auto fast = [&](const int n, auto slot) {
@@ -521,12 +517,31 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : (NCG =
         }
         stamp(6);
     };
+    // step n is fast when n != next_act, n < q_hi, n < n_hi, the plan is fused with <= 4 outputs, and no live
+    // trajectory is inactive (n < act), unfused (!fz) or has an MTO at n or n + 1. Fast steps change none of these,
+    // so the first step >= n that is not fast is found once, with one wave-wide minimum, instead of two ballots
+    // per pair
+    auto fast_end = [&](const int n) -> int {
+        if (!(fuse && NO <= 4 && !(p.ablate & 31))) return n;
+        int e = INT_MAX;
+        if (traj >= 0) e = (n < act || !fz) ? n : (evn.x >= n ? (evn.x - 1 > n ? evn.x - 1 : n) : INT_MAX);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const int y = __shfl_xor(e, o);
+            e = y < e ? y : e;
+        }
+        e = __builtin_amdgcn_readfirstlane(e);
+        if (next_act >= n && next_act < e) e = next_act;
+        if (q_hi < e) e = q_hi;
+        if (n_hi < e) e = n_hi;
+        return e < n ? n : e;
+    };
     for (int n = n0;; ++n) {
         // runs of fast step PAIRS in a loop of their own, one straight-line body over the two ring slots (slot 0
         // holds step n, slot 1 step n + 1 at the top of every pair; each slot fetches two steps ahead, no register
-        // moves, so the compiler's wait counts never drain a fetch early). A fast step leaves the state fast_ok
-        // reads unchanged, so both steps of a pair are checked up front; an odd step left over takes step()
-        while (fast_ok(n) && fast_ok(n + 1)) {
+        // moves, so the compiler's wait counts never drain a fetch early); an odd step left over takes step()
+        const int fe = fast_end(n);
+        while (n + 1 < fe) {
             fast(n, std::integral_constant<int, 0>{});
             fast(n + 1, std::integral_constant<int, 1>{});
             n += 2;
