@@ -159,28 +159,35 @@ def cpu_threads(info):
     return max(1, n)
 
 
+CPU_BLOCK = 8   # trajectories per lockstep block of the CPU port (oracle/pqd_oracle_blk.c)
+
+
 def cpu_baseline(chi, target_s=15.0):
-    """oracle/liboracle.so (plain-C port, OpenMP over trajectories) on a bounded sample of the same workload"""
+    """the CPU port on a bounded sample of the same workload: oracle/pqd_oracle_blk.c (the oracle's algorithm with
+    trajectories advanced in lockstep blocks of CPU_BLOCK, so every slice row read serves the whole block; OpenMP
+    over blocks), checked against the plain oracle in tests/test_oracle_blocked.py"""
     from oracle import oracle
     info = host_cpu()
     threads = cpu_threads(info)
+    unit = threads * CPU_BLOCK        # trajectories per round of blocks over all threads
     # calibrate on the same shape with all threads (setup + free propagators included, as in the sample)
-    n_traj = 2 * threads
+    n_traj = unit
     sysd, grid, pt, rho0, ops, tr = build_workload(n_traj, 300, chi)
     t0 = time.perf_counter()
-    oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt, nthreads=threads)
+    oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt, nthreads=threads, blocked=CPU_BLOCK)
     per = (time.perf_counter() - t0) / float(np.sum(tr.out_end + 1))  # seconds per traj-step
     total = target_s / per                                   # traj-steps that fill ~target_s
     steps = int(max(50, min(10000, total / n_traj)))
-    n_traj = int(min(4096, max(n_traj, threads * round(total / steps / threads))))
+    n_traj = int(min(4096, max(unit, unit * round(total / steps / unit))))
     sysd, grid, pt, rho0, ops, tr = build_workload(n_traj, steps, chi)
     t0 = time.perf_counter()
-    oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt, nthreads=threads)
+    oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt, nthreads=threads, blocked=CPU_BLOCK)
     el = time.perf_counter() - t0
     executed = int(np.sum(tr.out_end + 1))
     return {"value": executed / el, "unit": "traj-steps/s", "cores": threads, "kind": "port", "host": info,
             "sample": f"{n_traj} trajectories x {steps} tau-steps (executed {executed} traj-steps incl. trunk and "
-                      f"free-propagator build), chi={chi}, N=4, {el:.1f} s, oracle/pqd_oracle.c OpenMP"}
+                      f"free-propagator build), chi={chi}, N=4, {el:.1f} s, oracle/pqd_oracle_blk.c OpenMP over "
+                      f"lockstep blocks of {CPU_BLOCK} trajectories"}
 
 
 def main():

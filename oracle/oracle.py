@@ -53,6 +53,7 @@ def lib():
             build()
         _lib = C.CDLL(LIB)
         _lib.or_propagate.restype = C.c_int
+        _lib.or_propagate_blocked.restype = C.c_int
         _lib.or_free_propagators.restype = C.c_int
     return _lib
 
@@ -110,9 +111,10 @@ def expm(A):
     return E
 
 
-def propagate(system, grid, rho0, out_ops, traj, pt=None, M=None, nthreads=1):
+def propagate(system, grid, rho0, out_ops, traj, pt=None, M=None, nthreads=1, blocked=0):
     """Same contract as pyaceqd_amd.engine.propagate (list of (window, n_out) arrays); a list of systems
-    with traj.system is handled by running each system's trajectories separately."""
+    with traj.system is handled by running each system's trajectories separately. blocked = bt > 0 runs
+    or_propagate_blocked (pqd_oracle_blk.c: lockstep blocks of bt trajectories, bench.py's CPU baseline)."""
     from pyaceqd_amd.engine import split_output, Trajectories
     if isinstance(system, (list, tuple)):
         res = [None] * traj.n_traj
@@ -125,7 +127,7 @@ def propagate(system, grid, rho0, out_ops, traj, pt=None, M=None, nthreads=1):
             sub = Trajectories(np.asarray(traj.out_begin)[ids], np.asarray(traj.out_end)[ids],
                                [type(m)(remap[m.traj], m.step, m.before, m.kind, m.op) for m in traj.mtos
                                 if m.traj in remap])
-            for i, r in zip(ids, propagate(sy, grid, rho0, out_ops, sub, pt=pt, nthreads=nthreads)):
+            for i, r in zip(ids, propagate(sy, grid, rho0, out_ops, sub, pt=pt, nthreads=nthreads, blocked=blocked)):
                 res[i] = r
         return res
     keep = []
@@ -164,8 +166,9 @@ def propagate(system, grid, rho0, out_ops, traj, pt=None, M=None, nthreads=1):
         M = _c(M)
         keep.append(M)
         Mp = _p(M)
-    rc = lib().or_propagate(C.byref(s), C.byref(g), C.byref(ptc) if ptc is not None else None, _p(r0), C.c_int(n_out),
-                            _p(ops), C.byref(t), Mp, _p(out), C.c_int(nthreads))
+    args = (C.byref(s), C.byref(g), C.byref(ptc) if ptc is not None else None, _p(r0), C.c_int(n_out), _p(ops),
+            C.byref(t), Mp, _p(out), C.c_int(nthreads))
+    rc = lib().or_propagate_blocked(*args, C.c_int(blocked)) if blocked > 0 else lib().or_propagate(*args)
     assert rc == 0
     return split_output(out, traj, n_out)
 

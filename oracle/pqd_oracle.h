@@ -90,6 +90,11 @@ int or_propagate(const or_system* sys, const or_grid* g, const or_pt* pt, const 
                  int n_out, const ocplx* out_ops, const or_traj* tr, const ocplx* M,
                  ocplx* out, int nthreads);
 
+/* the same propagation with trajectories advanced in lockstep blocks of bt (pqd_oracle_blk.c): bench.py's CPU
+ * baseline; agrees with or_propagate to rounding */
+int or_propagate_blocked(const or_system* sys, const or_grid* g, const or_pt* pt, const ocplx* rho0, int n_out,
+                         const ocplx* out_ops, const or_traj* tr, const ocplx* M, ocplx* out, int nthreads, int bt);
+
 /* ---- Fortran map-chain sweeps (restated one-to-one, mapchain_oracle.c) ---- */
 void or_propagate_tau(const ocplx* dm_tl, const ocplx* rho_init, int n_tau, int dim, int j_start,
                       ocplx* rho_out);

@@ -52,7 +52,8 @@ def test_oracle_under_asan():
     which = subprocess.run([sys.executable, "-c", "from oracle import oracle; oracle.lib(); print(oracle.LIB)"],
                            cwd=REPO, env=env, capture_output=True, text=True, timeout=120)
     assert which.stdout.strip().endswith("liboracle_asan.so"), which.stdout + which.stderr
-    out = _run_under_asan({"PQD_ORACLE_LIB": lib}, ["tests/test_oracle_golden.py", "tests/test_oracle_physics.py"], 600)
+    out = _run_under_asan({"PQD_ORACLE_LIB": lib}, ["tests/test_oracle_golden.py", "tests/test_oracle_physics.py",
+                                                        "tests/test_oracle_blocked.py"], 600)
     assert "passed" in out
 
 
