@@ -54,27 +54,32 @@ static void mto_strided(int N, int chi, ocplx* st, size_t rs, int kind, const oc
     }
 }
 
-/* nw[a2][:] = sum_a M[a2][a] st[a][:], rows of len = bt chi contiguous */
+/* nw[a2][:] = sum_a M[a2][a] st[a][:], rows of len = bt chi contiguous; in column chunks of FB so the N^2 input
+ * and output row pieces of a chunk stay in L1 (a pass over whole rows per output row would stream the block state
+ * from L2 N^2 times per half step) */
+#define FB 64
 static void free_block(int N2, size_t len, const ocplx* M, const ocplx* st, ocplx* nw) {
-    for (int a2 = 0; a2 < N2; ++a2) {
-        ocplx* o = nw + (size_t)a2 * len;
-        const ocplx* m = M + (size_t)a2 * N2;
-        int a = 0;
-        {
-            const ocplx m0 = m[0];
-            const ocplx* s0 = st;
-            for (size_t j = 0; j < len; ++j) o[j] = m0 * s0[j];
-            a = 1;
-        }
-        for (; a + 3 <= N2; a += 3) {
-            const ocplx m0 = m[a], m1 = m[a + 1], m2 = m[a + 2];
-            const ocplx *s0 = st + (size_t)a * len, *s1 = s0 + len, *s2 = s1 + len;
-            for (size_t j = 0; j < len; ++j) o[j] += m0 * s0[j] + m1 * s1[j] + m2 * s2[j];
-        }
-        for (; a < N2; ++a) {
-            const ocplx m0 = m[a];
-            const ocplx* s0 = st + (size_t)a * len;
-            for (size_t j = 0; j < len; ++j) o[j] += m0 * s0[j];
+    for (size_t j0 = 0; j0 < len; j0 += FB) {
+        const size_t jn = (len - j0) < FB ? (len - j0) : FB;
+        for (int a2 = 0; a2 < N2; ++a2) {
+            ocplx* o = nw + (size_t)a2 * len + j0;
+            const ocplx* m = M + (size_t)a2 * N2;
+            {
+                const ocplx m0 = m[0];
+                const ocplx* s0 = st + j0;
+                for (size_t j = 0; j < jn; ++j) o[j] = m0 * s0[j];
+            }
+            int a = 1;
+            for (; a + 3 <= N2; a += 3) {
+                const ocplx m0 = m[a], m1 = m[a + 1], m2 = m[a + 2];
+                const ocplx *s0 = st + (size_t)a * len + j0, *s1 = s0 + len, *s2 = s1 + len;
+                for (size_t j = 0; j < jn; ++j) o[j] += m0 * s0[j] + m1 * s1[j] + m2 * s2[j];
+            }
+            for (; a < N2; ++a) {
+                const ocplx m0 = m[a];
+                const ocplx* s0 = st + (size_t)a * len + j0;
+                for (size_t j = 0; j < jn; ++j) o[j] += m0 * s0[j];
+            }
         }
     }
 }
