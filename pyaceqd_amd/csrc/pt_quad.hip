@@ -428,8 +428,9 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : (NCG =
     // matrix cores, exchange + barrier, A-operand reads, the contraction.
     // ring slot S (compile time): step n's operands; after use the slot fetches step n + 2 (no register moves,
     // so each fetch has two steps to arrive; see the loop below)
-    auto fast = [&](const int n, auto slot) {
+    auto fast = [&](const int n, auto slot, auto reload) {
         constexpr int S = decltype(slot)::value;
+        constexpr bool RL = decltype(reload)::value;  // false: the schedule keeps this slice and closure at n + 1
         auto stamp = [&](int k) {
             if constexpr (STAMP) {
                 if (blockIdx.x == 0 && threadIdx.x == 0 && n >= 1000 && n < 1016)
@@ -485,7 +486,7 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : (NCG =
                 p.out[wo2 + (long long)(n - wb2) * NO + k2] = x;
         }
         // ring loads of step n + 2 into the slot this step used
-        const int s1 = __builtin_amdgcn_readfirstlane(sr[S]);  // sched[n + 1]
+        const int s1 = RL ? __builtin_amdgcn_readfirstlane(sr[S]) : q_cur;  // sched[n + 1]
         fpre[S] = ldF(n + 2);
         ldW(S, n + 2);
         sr[S] = ldS(n + 3);
@@ -510,12 +511,25 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : (NCG =
         // a new slice (or closure) for step n + 1 only when the schedule changes. The wait sits inside the branch: a
         // load that MAY be in flight at the join makes the compiler wait for every older load at the first use
         // (vmcnt counts in order), i.e. for the ring fetches of step n + 2 just issued, on every step
-        if (q_cur != c_cur || s1 != q_cur) {
-            if (q_cur != c_cur) { load_closure(q_cur); c_cur = q_cur; }
-            if (s1 != q_cur) { load_slices(s1); q_cur = s1; }
-            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        if constexpr (RL) {
+            if (q_cur != c_cur || s1 != q_cur) {
+                if (q_cur != c_cur) { load_closure(q_cur); c_cur = q_cur; }
+                if (s1 != q_cur) { load_slices(s1); q_cur = s1; }
+                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+            }
         }
         stamp(6);
+    };
+    // the first step m in (n, lim) whose slice differs from step n's (lim if none): steps n .. m - 2 need no
+    // reload check when the closure has caught up (q_cur == c_cur)
+    auto same_end = [&](const int n, const int lim) -> int {
+        const int s0 = p.sched[n];
+        for (int m0 = n + 1; m0 < lim; m0 += 64) {
+            const int m = m0 + lane;
+            const unsigned long long b = __ballot(m < lim && p.sched[m] != s0);
+            if (b) return m0 + (int)__builtin_ctzll(b);
+        }
+        return lim;
     };
     // step n is fast when n != next_act, n < q_hi, n < n_hi, the plan is fused with <= 4 outputs, and no live
     // trajectory is inactive (n < act), unfused (!fz) or has an MTO at n or n + 1. Fast steps change none of these,
@@ -542,9 +556,19 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : (NCG =
         // moves, so the compiler's wait counts never drain a fetch early); an odd step left over takes step()
         const int fe = fast_end(n);
         while (n + 1 < fe) {
-            fast(n, std::integral_constant<int, 0>{});
-            fast(n + 1, std::integral_constant<int, 1>{});
-            n += 2;
+            // a repeated slice (ACE's _repeated / infinite PTs) leaves the schedule constant for long runs: pairs
+            // inside such a run skip the reload check and its wait for the schedule fetch
+            const int se = q_cur == c_cur ? same_end(n, fe + 1 < ns ? fe + 1 : ns) : n;
+            while (n + 2 < se && n + 1 < fe) {
+                fast(n, std::integral_constant<int, 0>{}, std::false_type{});
+                fast(n + 1, std::integral_constant<int, 1>{}, std::false_type{});
+                n += 2;
+            }
+            if (n + 1 < fe) {
+                fast(n, std::integral_constant<int, 0>{}, std::true_type{});
+                fast(n + 1, std::integral_constant<int, 1>{}, std::true_type{});
+                n += 2;
+            }
         }
         if (step(n)) break;
     }

@@ -1,7 +1,7 @@
 #!/bin/bash
 # quad kernel: fast-run end found once per entry (tree) vs two ballots per pair (ab/libpqd_base.so); parity, C2 A/B
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
-O=gpurun_out/quad_fe; mkdir -p $O
+O=gpurun_out/quad_fe2; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_quad.py tests/test_gpu_branching.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
 rc=$?; tail -2 $O/pytest.log; case $rc in 0) ;; *) grep -E "^FAILED|Error|assert" $O/pytest.log | head; echo "rc=$rc stop"; exit 1;; esac
