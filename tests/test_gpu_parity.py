@@ -133,12 +133,12 @@ def test_sweep_pt_split_full_c3_single_run(monkeypatch):
 
 
 @pytest.mark.parametrize("fpm", ["0", "1"])
-@pytest.mark.parametrize("N,n_sub,dt", [(4, 1, 0.1), (4, 2, 1.0), (4, 1, 2.0), (5, 1, 0.1), (5, 2, 1.0), (6, 1, 0.1),
-                                        (6, 1, 1.0), (6, 3, 2.0)])
+@pytest.mark.parametrize("N,n_sub,dt", [(2, 1, 0.1), (2, 2, 1.0), (2, 3, 2.0), (2, 1, 5.0), (4, 1, 0.1), (4, 2, 1.0),
+                                        (4, 1, 2.0), (5, 1, 0.1), (5, 2, 1.0), (6, 1, 0.1), (6, 1, 1.0), (6, 3, 2.0)])
 def test_free_propagators_large_n_mfma_and_lds(monkeypatch, fpm, N, n_sub, dt):
     """N2 = 16 / 25 / 36 on the matrix-core kernel (free_prop_mfma_kernel, 4 x 4 blocks, 25 padded to 28) and on
-    the LDS kernel (PQD_FPM=0), vs the oracle: norms from ~0.5 to several (dt = 1, 2: squarings), sub-steps (Acc
-    products)"""
+    the LDS kernel (PQD_FPM=0), vs the oracle: norms from ~0.5 to several (dt = 1, 2, 5: squarings), sub-steps (Acc
+    products). N2 = 4 runs the packed 4 x 4 kernel (free_prop4_kernel) under either setting"""
     monkeypatch.setenv("PQD_FPM", fpm)
     sysd, grid = H.random_system(N, n_steps=12, n_sub=n_sub, dt=dt, seed=7 * N + n_sub)
     got = engine.free_propagators(sysd, grid)
