@@ -513,13 +513,100 @@ static int fp4_chunk(const FreePropParams& p) {
     return 16 * (int)(g < 1 ? 1 : (g > 8 ? 8 : g));
 }
 
+// The same propagator on the FP64 matrix cores: one v_mfma_f64_4x4x4_4b carries the 4 x 4 products of the wave's
+// four matrices (block g = matrix), three instructions per complex product (3M). Lane l = 16 i + 4 g + j holds
+// element (i, j) of matrix g: the instruction's D-layout, which is also the B-layout of the next product, so Horner
+// steps chain without data movement; the A operand (lane 16 k + 4 g + i holds element (i, k)) is one shuffle of a
+// D-layout value, done once per sub-step for the scaled generator and once per squaring. Degrees and squaring counts
+// stay per matrix (the wave runs to its largest and each matrix keeps its value past its own count), so a matrix
+// gets exactly the polynomial and squarings of fp4_matrix; only the rounding of the products differs (3M).
+__device__ __forceinline__ double2 mm4_mfma(double2 aA, double2 b) {
+    const double p1 = __builtin_amdgcn_mfma_f64_4x4x4f64(aA.x, b.x, 0.0, 0, 0, 0);
+    const double p2 = __builtin_amdgcn_mfma_f64_4x4x4f64(aA.y, b.y, 0.0, 0, 0, 0);
+    const double p3 = __builtin_amdgcn_mfma_f64_4x4x4f64(aA.x + aA.y, b.x + b.y, 0.0, 0, 0, 0);
+    return make_double2(p1 - p2, p3 - p1 - p2);
+}
+// D-layout -> A-layout: lane (k, g, i) takes element (i, k) of matrix g, held by lane 16 i + 4 g + k
+__device__ __forceinline__ double2 to_a4(double2 v, int lane) {
+    return c_shfl(v, 16 * (lane & 3) + (lane & 12) + (lane >> 4));
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) { const int y = __shfl_xor(v, o); v = y > v ? y : v; }
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
+// all 64 lanes of the wave call this together (the MFMAs read every lane); matrix g = (lane >> 2) & 3
+__device__ __forceinline__ void fp4m_matrix(const FreePropParams& p, int si, int m, bool live, int lane) {
+    const int n = m >> 1, h = m & 1;
+    const int i = lane >> 4, j = lane & 3, e = 4 * i + j;
+    const FreePropSys sy = p.systems[si];
+    const int nsub = p.n_sub > 0 ? p.n_sub : 1;
+    const double w = 0.5 * p.dt / nsub;
+    double2* out = p.idle_pass ? p.Midle + (size_t)si * 16 : p.M + ((size_t)si * 2 * p.n_steps + m) * 16;
+    const bool idle = !p.idle_pass && p.Midle && idle_half_step(sy, p.ta + n * p.dt + h * 0.5 * p.dt, w, nsub);
+    if (idle && live) out[e] = p.Midle[(size_t)si * 16 + e];
+    if (__ballot(!idle) == 0) return;  // wave-uniform
+    double2 acc = c_zero();
+    for (int js = 0; js < nsub; ++js) {
+        const double t = p.ta + n * p.dt + h * 0.5 * p.dt + (js + 0.5) * w;
+        double2 v = sy.L0[e];
+        for (int c = 0; c < sy.n_chan && c < 4; ++c) {
+            const double2 f = p.idle_pass ? c_zero() : sample_ch(sy, c, t);
+            c_fma(v, f, sy.S[(size_t)c * 16 + e]);
+            c_fma(v, c_conj(f), sy.T[(size_t)c * 16 + e]);
+        }
+        double2 a = c_scale(v, w);
+        // 1-norm as fp4_matrix: column sums in row order, then the max over columns
+        double cs = 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { const double2 x = c_shfl(a, 16 * r + (lane & 15)); cs += hypot(x.x, x.y); }
+        double norm = 0.0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) { const double x = __shfl(cs, (lane & ~3) + c); norm = x > norm ? x : norm; }
+        int e2 = 0;
+        frexp(norm / 0.5, &e2);
+        const int sh = e2 > 0 ? e2 : 0;
+        const double theta = ldexp(norm, -sh);
+        double rem = 0.5 * theta * theta;
+        int deg = 1;
+        while (deg < 18 && rem * 1.7 > 1.4e-17) { ++deg; rem *= theta / (deg + 1); }
+        a = c_scale(a, ldexp(1.0, -sh));
+        const double2 aA = to_a4(a, lane);
+        double2 pm = make_double2(a.x / (double)deg, a.y / (double)deg);
+        if (i == j) pm.x += 1.0;
+        const int dmax = wave_max_i(deg), smax = wave_max_i(sh);
+        for (int mm = dmax - 1; mm >= 1; --mm) {
+            const double2 tv = mm4_mfma(aA, pm);
+            double2 u = make_double2(tv.x / (double)mm, tv.y / (double)mm);
+            if (i == j) u.x += 1.0;
+            const bool up = mm < deg;  // per-component selects (a select of double2 values went through scratch)
+            pm.x = up ? u.x : pm.x;
+            pm.y = up ? u.y : pm.y;
+        }
+        for (int q = 0; q < smax; ++q) {
+            const double2 tv = mm4_mfma(to_a4(pm, lane), pm);
+            const bool up = q < sh;
+            pm.x = up ? tv.x : pm.x;
+            pm.y = up ? tv.y : pm.y;
+        }
+        if (js == 0) acc = pm;
+        else acc = mm4_mfma(to_a4(pm, lane), acc);
+    }
+    if (live && !idle) out[e] = acc;
+}
+
+template <bool MF>
 __global__ __launch_bounds__(256) void free_prop4_kernel(FreePropParams p) {
     const int tid = threadIdx.x, lane = tid & 63;
+    // matrix of this lane within the workgroup's 16: 16-lane groups (fp4_matrix) or block g of the wave (fp4m_matrix)
+    const int mw = MF ? 4 * (tid >> 6) + ((lane >> 2) & 3) : tid >> 4;
     if (p.idle_pass) {
         for (long long base = (long long)blockIdx.x * 16; base < p.n_sys; base += (long long)gridDim.x * 16) {
-            const long long mat = base + (tid >> 4);
+            const long long mat = base + mw;
             const bool live = mat < p.n_sys;
-            fp4_matrix(p, (int)(live ? mat : p.n_sys - 1), 0, live, lane);
+            if constexpr (MF) fp4m_matrix(p, (int)(live ? mat : p.n_sys - 1), 0, live, lane);
+            else fp4_matrix(p, (int)(live ? mat : p.n_sys - 1), 0, live, lane);
         }
         return;
     }
@@ -537,9 +624,10 @@ __global__ __launch_bounds__(256) void free_prop4_kernel(FreePropParams p) {
             hi = hi < wn.y ? hi : wn.y;
         }
         for (int base = lo; base <= hi; base += 16) {
-            const int m = base + (tid >> 4);
+            const int m = base + mw;
             const bool live = m <= hi;
-            fp4_matrix(p, si, live ? m : hi, live, lane);
+            if constexpr (MF) fp4m_matrix(p, si, live ? m : hi, live, lane);
+            else fp4_matrix(p, si, live ? m : hi, live, lane);
         }
     }
 }
@@ -823,8 +911,13 @@ static hipError_t launch_free_prop_pass(int N2, const FreePropParams& p, hipStre
         const long long nblk = p.idle_pass ? ((long long)p.n_sys + 15) / 16
                                            : (long long)p.n_sys * ((2LL * p.n_steps + q.chunk - 1) / q.chunk);
         if (nblk <= 0) return hipSuccess;
-        hipLaunchKernelGGL(free_prop4_kernel, dim3((unsigned)std::min<long long>(nblk, FP_MAX_BLOCKS)), dim3(256), 0, s,
-                           q);
+        // p.mfma (PQD_FPM, default 1): the matrix-core products; 0: the shuffle products (A/B)
+        if (p.mfma)
+            hipLaunchKernelGGL(free_prop4_kernel<true>, dim3((unsigned)std::min<long long>(nblk, FP_MAX_BLOCKS)), dim3(256),
+                               0, s, q);
+        else
+            hipLaunchKernelGGL(free_prop4_kernel<false>, dim3((unsigned)std::min<long long>(nblk, FP_MAX_BLOCKS)),
+                               dim3(256), 0, s, q);
         return hipGetLastError();
     }
     switch (N2) {

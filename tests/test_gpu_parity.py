@@ -138,7 +138,8 @@ def test_sweep_pt_split_full_c3_single_run(monkeypatch):
 def test_free_propagators_large_n_mfma_and_lds(monkeypatch, fpm, N, n_sub, dt):
     """N2 = 16 / 25 / 36 on the matrix-core kernel (free_prop_mfma_kernel, 4 x 4 blocks, 25 padded to 28) and on
     the LDS kernel (PQD_FPM=0), vs the oracle: norms from ~0.5 to several (dt = 1, 2, 5: squarings), sub-steps (Acc
-    products). N2 = 4 runs the packed 4 x 4 kernel (free_prop4_kernel) under either setting"""
+    products). N2 = 4: the packed kernel's matrix-core products (four matrices per wave, each with its own degree and
+    squaring count) and its shuffle products (PQD_FPM=0)"""
     monkeypatch.setenv("PQD_FPM", fpm)
     sysd, grid = H.random_system(N, n_steps=12, n_sub=n_sub, dt=dt, seed=7 * N + n_sub)
     got = engine.free_propagators(sysd, grid)
