@@ -47,6 +47,12 @@ __device__ __forceinline__ bool idle_half_step(const FreePropSys& sy, double t0,
     return true;
 }
 
+// 1 / mm for the Horner steps of the matrix-core builders: a wave-uniform index reads it with a scalar load, where a
+// division is a dozen FP64 VALU instructions per element (and FP64 VALU does not co-issue with the matrix cores).
+// x * (1 / mm) may differ from x / mm in the last place; parity vs the oracle is at 1e-12 relative
+__constant__ double k_rinv[19] = {0.0, 1.0, 1.0 / 2, 1.0 / 3, 1.0 / 4, 1.0 / 5, 1.0 / 6, 1.0 / 7, 1.0 / 8, 1.0 / 9,
+                                  1.0 / 10, 1.0 / 11, 1.0 / 12, 1.0 / 13, 1.0 / 14, 1.0 / 15, 1.0 / 16, 1.0 / 17, 1.0 / 18};
+
 template <int N2>
 __device__ __forceinline__ void lds_matmul(const double2* A, const double2* B, double2* C, int tid) {
     if constexpr (N2 == 36) {
@@ -360,6 +366,7 @@ __global__ __launch_bounds__(256) void free_prop_mfma_kernel(FreePropParams p) {
             __syncthreads();
             // Horner: P <- A P / mm + I
             for (int mm = deg - 1; mm >= 1; --mm) {
+                const double rm = k_rinv[mm];
                 fpm_product<N2>(A, P, R, wave, lane);
                 __syncthreads();
 #pragma unroll
@@ -367,7 +374,7 @@ __global__ __launch_bounds__(256) void free_prop_mfma_kernel(FreePropParams p) {
                     int r, c;
                     const int ix = fpm_index<N2>(q, wave, lane, r, c);
                     if (ix >= 0) {
-                        double2 pv = make_double2(R[q].x / (double)mm, R[q].y / (double)mm);
+                        double2 pv = make_double2(R[q].x * rm, R[q].y * rm);
                         if (r == c) pv.x += 1.0;
                         P[ix] = pv;
                     }
@@ -578,7 +585,8 @@ __device__ __forceinline__ void fp4m_matrix(const FreePropParams& p, int si, int
         const int dmax = wave_max_i(deg), smax = wave_max_i(sh);
         for (int mm = dmax - 1; mm >= 1; --mm) {
             const double2 tv = mm4_mfma(aA, pm);
-            double2 u = make_double2(tv.x / (double)mm, tv.y / (double)mm);
+            const double rm = k_rinv[mm];
+            double2 u = make_double2(tv.x * rm, tv.y * rm);
             if (i == j) u.x += 1.0;
             const bool up = mm < deg;  // per-component selects (a select of double2 values went through scratch)
             pm.x = up ? u.x : pm.x;
