@@ -252,6 +252,24 @@ int pqd_dynamics_t1(pqd_ctx* ctx, const pqd_c128* dm_1, const pqd_c128* dm_2, co
 int pqd_tl_dynmap_pseudo(pqd_ctx* ctx, const pqd_c128* dm, int32_t n_maps, int32_t n, double rcond,
                          pqd_c128* out);
 
+/* ---- PT generator factorizations (replaces the factorizations inside `ACE <generate.param>` with
+ * `dont_propagate true` + `write_PT`, reference general_system.py:152-211; driven by pyaceqd_amd/ptgen_gpu.py,
+ * whose host restatement is pyaceqd_amd/ptgen.py). Device pointers, column-major matrices (ld = rows), all work
+ * enqueued on `stream` (a hipStream_t); both calls return after one device synchronisation (the rank / sweep
+ * count decides what the caller does next).
+ *
+ * pqd_ptg_qr: Householder QR of W (m x n, overwritten). pivot = 0: W = Q R with rank = min(m, n) (LAPACK zgeqrf
+ * reflectors, R real diagonal). pivot = 1: column pivoting on the trailing column norms, stopping at the first step
+ * whose largest trailing column norm is <= tol (a rank-revealing truncation): W P ~= Q R. Outputs: Q (m x rank),
+ * R (rank x n, columns in pivoted order), perm (n: column j of W P is column perm[j] of W), *rank (host). */
+int pqd_ptg_qr(void* stream, pqd_c128* W, int32_t m, int32_t n, int32_t pivot, double tol, pqd_c128* Q,
+               pqd_c128* R, int32_t* perm, int32_t* rank);
+/* pqd_ptg_jacobi: one-sided Jacobi SVD of a square n x n X (overwritten): X V = U diag(sigma), columns rotated
+ * until every pair satisfies |x_p^H x_q| <= tol |x_p| |x_q|. Outputs: X <- U (unit columns, unsorted), V (n x n),
+ * sigma (n, unsorted), *sweeps (host). */
+int pqd_ptg_jacobi(void* stream, pqd_c128* X, int32_t n, pqd_c128* V, double* sigma, double tol,
+                   int32_t max_sweeps, int32_t* sweeps);
+
 #ifdef __cplusplus
 }
 #endif

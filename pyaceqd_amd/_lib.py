@@ -14,7 +14,10 @@ LIB_PATH = os.environ.get("PQD_LIB") or os.path.join(_HERE, "libpqd.so")  # PQD_
 
 
 class PQDError(RuntimeError):
-    pass
+    code = None  # the PQD_ERR_* status that raised it
+
+
+PQD_ERR_UNSUPPORTED = 3
 
 
 class NumericError(PQDError):
@@ -117,6 +120,11 @@ _SIGS = {
     "pqd_dynamics_t1": ([C.c_void_p, P_C128, P_C128, P_C128, P_F64, P_C128, C.c_int32, C.c_double, C.c_int32,
                          C.c_int32, C.c_double, C.c_int32, P_C128], C.c_int),
     "pqd_tl_dynmap_pseudo": ([C.c_void_p, P_C128, C.c_int32, C.c_int32, C.c_double, P_C128], C.c_int),
+    # PT generator factorizations on device pointers (ptgen_gpu.py)
+    "pqd_ptg_qr": ([C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_double, C.c_void_p, C.c_void_p,
+                    C.c_void_p, P_I32], C.c_int),
+    "pqd_ptg_jacobi": ([C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_double, C.c_int32, P_I32],
+                       C.c_int),
 }
 
 EXPORTED = tuple(_SIGS)
@@ -145,7 +153,9 @@ def check(rc):
     if rc != 0:
         msg = lib().pqd_last_error().decode(errors="replace")
         exc = ValueError if rc == 1 else NumericError if rc == 5 else PQDError
-        raise exc(f"libpqd error {rc}: {msg}")
+        e = exc(f"libpqd error {rc}: {msg}")
+        e.code = rc  # the C-ABI status (include/pqd.h PQD_ERR_*)
+        raise e
 
 
 def cptr(a):

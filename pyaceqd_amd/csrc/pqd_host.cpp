@@ -203,7 +203,12 @@ void touch_pages(void* buf, size_t bytes) {
         for (size_t o = (size_t)k * chunk; o < std::min(bytes, (size_t)(k + 1) * chunk); o += 4096) q[o] = 0;
     };
     std::vector<std::thread> th;
-    for (int k = 1; k < nth; ++k) th.emplace_back(work, k);
+    int k_started = 1;
+    try {
+        for (; k_started < nth; ++k_started) th.emplace_back(work, k_started);
+    } catch (...) {  // no thread could be started: touch the remaining chunks here (no exception crosses the C-ABI)
+    }
+    for (int k = k_started; k < nth; ++k) work(k);
     work(0);
     for (auto& t : th) t.join();
 }
@@ -1375,6 +1380,10 @@ static int mapchain_run(pqd_ctx* ctx, MapChainParams& p, const pqd_c128* dmA, si
             p.q_s = any_s ? qp : INT_MAX;
             for (int i = 0; i < p.n_t; ++i)
                 if (pos[i] + 1 > p.n_tb) pos[i] = p.q_s;
+            // precondition of that constant region: with n_map > n_tb a trunk ending at n_tb < j <= n_map walks
+            // dm_block(j), dm_block(j+1), ..., dm_block(n_map) before dm_s (:270-281), which the blocked position
+            // map does not represent; such calls run on the map-by-map kernels
+            if (any_s && p.n_map > p.n_tb) blocked = false;
         }
     }
     if (blocked) {
@@ -1431,7 +1440,11 @@ static int mapchain_run(pqd_ctx* ctx, MapChainParams& p, const pqd_c128* dmA, si
     // the caller's result array is typically fresh (f2py-style: np.zeros, pages not yet mapped): fault its pages in
     // on a few host threads while the maps upload and the kernels run, so the copy back runs at the link rate (a
     // 41 MB copy into fresh pages: 1.7 ms, into mapped ones 0.73 ms; scripts/ubench_h2d.py)
-    std::thread toucher(touch_pages, (void*)result, nres * sizeof(double2));
+    std::thread toucher;
+    try {
+        toucher = std::thread(touch_pages, (void*)result, nres * sizeof(double2));
+    } catch (...) {  // thread creation failed: skip the pre-touch (the copy back is only slower), never throw
+    }
     struct Join {
         std::thread& t;
         ~Join() { if (t.joinable()) t.join(); }

@@ -22,11 +22,13 @@ choice is a documented switch):
     Gaussian-bath PT is generated from the same parameters as ACE's generate file (pyaceqd_amd.ptgen) and cached.
 """
 import os
+import warnings
 
 import numpy as np
 
 from ..constants import hbar
 from .. import constants
+from .._lib import PQDError, PQD_ERR_UNSUPPORTED
 from .. import opgrammar
 from ..engine import Grid, MTO, ProcessTensor, System, Trajectories, free_propagators, propagate, propagate_table, \
     propagate_trapz, KIND
@@ -140,7 +142,15 @@ def _resolve_pt(pt_file, boson_mat, *, dt, t_mem, ae, temperature, threshold, fa
         # ACE's own files (detected as the reference does, :153-156), read under layout ACE_PTB_V0 (ace_pt.py)
         if verbose:
             print("using pt_file " + pt_file)
-        return ace_pt.read_ace_pt(pt_file, boson_mat.shape[0], dt=dt)
+        try:
+            return ace_pt.read_ace_pt(pt_file, boson_mat.shape[0], dt=dt)
+        except PQDError as e:
+            if e.code != PQD_ERR_UNSUPPORTED:
+                raise
+            # a file in a layout other than ACE_PTB_V0 (e.g. one ACE itself wrote): not an error of the call, the
+            # PT is taken from the pqd container or generated as if no ACE file were there
+            warnings.warn("{}_initial is not in a layout this reader knows ({}); using the pqd PT instead"
+                          .format(pt_file, e))
     for cand in (pt_file, pt_file + ".npz"):
         if os.path.isfile(cand) and J_to_file is None:
             if verbose:
@@ -178,7 +188,7 @@ def system_ace_stream(t_start, t_end, *pulses, dt=0.01, phonons=False, t_mem=20.
                       prepare_only=False, LO_params=None, dressedstates=False, rf_op=None, rf_file=None,
                       firstonly=False, J_to_file=None, J_file=None, factor_ah=None, use_infinite=False,
                       print_H=False, calc_dynmap=False, rho0=None, get_M_t=None, trajectories=None, n_sub=1,
-                      device=None, pulse_sampling="exact", trapz=None):
+                      device=None, pulse_sampling="ace_file", trapz=None):
     """Propagate one trajectory (or a batch: `trajectories`) and return ACE's output table.
 
     Returns (1 + len(output_ops), n_t) complex, row 0 = time (general_system.py:104-110, 343).
@@ -188,12 +198,13 @@ def system_ace_stream(t_start, t_end, *pulses, dt=0.01, phonons=False, t_mem=20.
     "system_op" / "lindblad_ops" replacing the call's): a list of per-trajectory results, all propagated in one launch
     (one System per distinct drive and generator: parameter scans over pulses and fields).
 
-    pulse_sampling: "exact" (default) samples the analytic pulses at dt/(4 n_sub), so every exponential midpoint
-    is a sample. "ace_file" gives the pulses the semantics of the files the reference hands ACE
-    (general_system.py:55-71, 213-223): samples on np.arange(t_start, t_end, dt) quantised to %.8f, linearly
-    interpolated between samples and held past t_end - dt, exactly as an explicit pulse_file_x/_y is read (and
-    the rf frequency likewise, :73-84). The two differ by O(dt^2 f'') (about 1e-4 relative for tau_0 = 3 ps at
-    dt = 0.1), which is above the no-phonon 1e-8 tolerance: use "ace_file" to compare against ACE output.
+    pulse_sampling: "ace_file" (default, the reference's input semantics) gives the pulses the semantics of the
+    files the reference hands ACE (general_system.py:55-71, 213-223): samples on np.arange(t_start, t_end, dt)
+    quantised to %.8f, linearly interpolated between samples and held past t_end - dt, exactly as an explicit
+    pulse_file_x/_y is read (and the rf frequency likewise, :73-84). "exact" (opt-in) samples the analytic pulses at
+    dt/(4 n_sub) instead, so every exponential midpoint is a sample of the analytic field. The two differ by
+    O(dt^2 f'') (about 1e-4 relative for tau_0 = 3 ps at dt = 0.1), above the no-phonon 1e-8 tolerance, which is
+    why the drop-in default is the reference's.
     """
     if pulse_sampling not in ("exact", "ace_file"):
         raise ValueError(f"pulse_sampling must be 'exact' or 'ace_file', not {pulse_sampling!r}")

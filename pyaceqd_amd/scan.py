@@ -51,11 +51,16 @@ def gather_tensor(local, dist=None, dst=0):
     copy of any block to the other ranks: at 8 ranks of 655 MB only rank 0 receives, 7 x 655 MB, where an all_gather
     would move 8 x 8 x 655 MB. Complex blocks travel as their real view. This is the one collective of a sharded
     sweep; the reference assembles its result lists from per-process CSV files
-    (correlations.py:171-183)."""
+    (correlations.py:171-183).
+
+    Round 3 changed this from an all-gather (the result on every rank) to a gather to `dst`: ranks other than `dst`
+    now get None. `all_gather_tensor` keeps the old result-on-every-rank behaviour."""
     import torch
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
         return local
     world, rank = dist.get_world_size(), dist.get_rank()
+    if not 0 <= dst < world:
+        raise ValueError(f"gather_tensor: dst {dst} outside [0, {world})")
     cplx = local.is_complex()
     x = (torch.view_as_real(local) if cplx else local).reshape(-1).contiguous()
     n = torch.tensor([x.numel()], dtype=torch.int64, device=x.device)
@@ -78,6 +83,23 @@ def gather_tensor(local, dist=None, dst=0):
     for q in reqs:
         q.wait()
     return torch.view_as_complex(out.reshape(-1, 2)) if cplx else out
+
+
+def all_gather_tensor(local, dist=None):
+    """Every rank's 1-D tensor concatenated in rank order on EVERY rank (gather_tensor to rank 0, then one broadcast
+    of the result): the pre-round-3 semantics of gather_tensor, for callers that use the result on all ranks."""
+    import torch
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return local
+    out = gather_tensor(local, dist, 0)
+    cplx = local.is_complex()
+    n = torch.tensor([0 if out is None else out.numel()], dtype=torch.int64, device=local.device)
+    dist.broadcast(n, 0)
+    if out is None:
+        out = torch.empty(int(n.item()), dtype=local.dtype, device=local.device)
+    buf = torch.view_as_real(out) if cplx else out
+    dist.broadcast(buf, 0)
+    return out
 
 
 def triangular_rows(n_t, rank, world):

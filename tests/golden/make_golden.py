@@ -373,7 +373,9 @@ def gen_twotime_anchor():
     fed to the REFERENCE tl_three_op_two_time / tl_two_op_two_time (use_dm=True; time-localised by the reference's
     calc_tl_dynmap_pseudo, swept by the reference's own Fortran or its row-major Python path). The GPU test runs our
     trajectory sweep `three_op_two_time` / `two_op_two_time` (MTOs at t1 inside the PT kernel) on the same model and
-    must reproduce these G within 1e-10."""
+    must reproduce these G within 1e-10. Both sides use the driver's default drive, pulse_sampling="ace_file" (the
+    reference's %.8f pulse files on np.arange(t_start, t_end, dt); regenerated in round 4 when that became the
+    default)."""
     import io
     import contextlib
     import warnings

@@ -13,7 +13,7 @@ import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from pyaceqd_amd.scan import gather_blocks, gather_tensor, run_sharded, shard_range
+from pyaceqd_amd.scan import all_gather_tensor, gather_blocks, gather_tensor, run_sharded, shard_range
 
 
 def test_shard_range_partitions():
@@ -84,7 +84,8 @@ def _gather_worker(rank, world, port, q):
     n = 3 + 4 * rank  # ragged blocks
     x = torch.arange(n, dtype=torch.float64) * (1 + 1j) + 100 * rank
     y = gather_tensor(x.to(torch.complex128), dist, dst=0)
-    q.put((rank, None if y is None else y.numpy()))
+    z = all_gather_tensor(x.to(torch.complex128), dist)
+    q.put((rank, (None if y is None else y.numpy(), z.numpy())))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -101,8 +102,9 @@ def test_gather_tensor_ragged_complex_world2():
         p.join(timeout=120)
         assert p.exitcode == 0
     ref = np.concatenate([np.arange(3 + 4 * r) * (1 + 1j) + 100 * r for r in range(2)])
-    assert np.array_equal(got[0], ref)  # gathered to rank 0 only
-    assert got[1] is None
+    assert np.array_equal(got[0][0], ref)  # gathered to rank 0 only
+    assert got[1][0] is None
+    assert np.array_equal(got[0][1], ref) and np.array_equal(got[1][1], ref)  # all_gather_tensor: on every rank
 
 
 N_T1, N_TAU, CHI = 16, 60, 16

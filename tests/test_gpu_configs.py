@@ -53,34 +53,45 @@ def _configs():
 
 
 # ------------------------------------------------------------------------------------------------ config 1
-def test_config1_tls_rabi_1000_steps(monkeypatch):
+@pytest.mark.parametrize("sampling", ["ace_file", "exact"])
+def test_config1_tls_rabi_1000_steps(monkeypatch, sampling):
+    """tls(0, 100, ...) through the driver (default pulse_sampling = "ace_file": the drive ACE reads from the
+    reference's %.8f pulse files) vs the oracle, and rho_11 vs a direct adaptive integration of the Lindblad equation
+    driven by the SAME field: the piecewise-linear interpolant of the %.8f samples on np.arange(0, 100, dt), held past
+    the last sample (general_system.py:55-71, 213), or the analytic pulse for pulse_sampling="exact"."""
     from scipy.integrate import solve_ivp
     from pyaceqd_amd.constants import hbar
     from pyaceqd_amd.pulses import ChirpedPulse
     from pyaceqd_amd.two_level_system.tls import tls
+    from pyaceqd_amd.general_system.general_system import _ace_file_samples, _sample_pulses
     p = ChirpedPulse(tau_0=3, e_start=0, e0=1, t0=20)
-    a = tls(0, 100, p, dt=0.1, lindblad=True)
+    a = tls(0, 100, p, dt=0.1, lindblad=True, pulse_sampling=sampling)
     assert a.shape == (5, 1001)
     assert np.max(np.abs(a[1] + a[2] - 1)) < 1e-12          # populations sum to one
     _oracle_patch(monkeypatch)
-    b = tls(0, 100, p, dt=0.1, lindblad=True)
+    b = tls(0, 100, p, dt=0.1, lindblad=True, pulse_sampling=sampling)
     assert np.max(np.abs(a - b)) < 1e-12
     # Lindblad master equation of the same model (tls.py:24-29 strings: H = -pi hbar/2 (f |1><0| + h.c.), decay
     # |0><1| at 1/100 per ps), integrated directly with an adaptive RK; the engine's symmetric Trotter steps at
     # dt = 0.1 differ by O(dt^2)
     g = 1 / 100
     s = np.array([[0, 1], [0, 0]], complex)      # |0><1|
+    if sampling == "ace_file":
+        tf, fx, _ = _ace_file_samples(np.arange(0, 100, 0.1), *_sample_pulses([p], np.arange(0, 100, 0.1)))
+        field = lambda t: complex(np.interp(t, tf, fx.real) + 1j * np.interp(t, tf, fx.imag))  # noqa: E731
+    else:
+        field = lambda t: complex(p.get_total(np.array([t]))[0])  # noqa: E731
 
     def rhs(t, y):
         r = y.reshape(2, 2)
-        f = complex(p.get_total(np.array([t]))[0])
+        f = field(t)
         X = -0.5 * np.pi * hbar * np.array([[0, 0], [1, 0]], complex)
         H = f * X + np.conj(f) * X.conj().T
         d = -1j / hbar * (H @ r - r @ H) + g * (s @ r @ s.conj().T - 0.5 * (s.conj().T @ s @ r + r @ s.conj().T @ s))
         return d.ravel()
     sol = solve_ivp(rhs, (0, 100), np.array([1, 0, 0, 0], complex), t_eval=[25.0, 40.0, 100.0], rtol=1e-11,
-                    atol=1e-13, method="DOP853")
-    exc = sol.y[3].real                            # rho_11 (measured: 0.95223, 0.82790, 0.45436; engine within 1e-6)
+                    atol=1e-13, method="DOP853", max_step=0.05 if sampling == "ace_file" else np.inf)
+    exc = sol.y[3].real        # rho_11 (measured: 0.95222, 0.82790, 0.45436; engine within 2.2e-7 ace_file, 6.7e-7 exact)
     assert np.max(np.abs(a[2][[250, 400, 1000]].real - exc)) < 1e-5
     assert exc[0] > 0.9                            # a pi pulse: the dot is inverted, then decays
 

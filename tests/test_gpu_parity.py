@@ -394,16 +394,19 @@ def test_mapchain_blocked_sweep_vs_oracle(monkeypatch, dim, L):
 
 @pytest.mark.parametrize("dim", [2, 4, 6])
 @pytest.mark.parametrize("L", ["8", "0"])
-def test_mapchain_blocked_sweep_block_mode_vs_oracle(monkeypatch, dim, L):
+@pytest.mark.parametrize("n_map", [7, 18])
+def test_mapchain_blocked_sweep_block_mode_vs_oracle(monkeypatch, dim, L, n_map):
     """calc_onetime_parallel_block on the blocked sweep: the periodic map sequence (dm_block for the first n_map of
     every n_tb, then dm_s), trunks ending inside and past the first period (those apply dm_s at every tau step,
-    propagate_tau.f90:270-287), vs the C oracle and the map-by-map kernel"""
+    propagate_tau.f90:270-287), vs the C oracle and the map-by-map kernel. n_map = 18 > n_tb = 12 puts trunk ends
+    inside (n_tb, n_map] (t1 = 1.2, 1.25: they walk dm_block(j..n_map) before dm_s), which the host routes to the
+    map-by-map kernels"""
     from pyaceqd_amd.two_time import propagate_tau_module as M
     if L != "0":
         monkeypatch.setenv("PQD_MC_L", L)
     rng = np.random.default_rng(10 + dim)
     N2 = dim * dim
-    n_map, n_tb, nx_tau = 7, 12, 9
+    n_tb, nx_tau = 12, 9
     mk = lambda: np.eye(N2) + 0.05 * (rng.normal(size=(N2, N2)) + 1j * rng.normal(size=(N2, N2))) / dim  # noqa
     dm_block = np.stack([mk() for _ in range(n_map)])
     dm_s = mk()
@@ -486,11 +489,15 @@ def _oracle_patch(monkeypatch):
                         engine.tables_from_outputs(prop(system, grid, rho0, out_ops, traj, pt), traj, grid))
 
 
-def test_tls_rabi_kat():
+@pytest.mark.parametrize("sampling", ["ace_file", "exact"])
+def test_tls_rabi_kat(sampling):
+    """area theorem: a resonant pulse of area pi e0 leaves sin^2(pi e0 / 2) in |1>. With the default ("ace_file",
+    the reference's %.8f files on np.arange(t_start, t_end, dt), linearly interpolated) the two half-step midpoints of
+    a step weigh the samples like the trapezoid rule, so the area is exact to the %.8f quantisation"""
     from pyaceqd_amd.two_level_system.tls import tls
     from pyaceqd_amd.pulses import ChirpedPulse
     for e0 in (0.5, 1.0, 2.0):
-        t, g, x, p, _ = tls(0, 40, ChirpedPulse(tau_0=3, e_start=0, e0=e0, t0=20), dt=0.05)
+        t, g, x, p, _ = tls(0, 40, ChirpedPulse(tau_0=3, e_start=0, e0=e0, t0=20), dt=0.05, pulse_sampling=sampling)
         assert abs(x[-1].real - np.sin(np.pi * e0 / 2) ** 2) < 1e-6
         assert np.max(np.abs(g + x - 1)) < 1e-12
 

@@ -116,3 +116,24 @@ def test_driver_generates_and_caches_pt(tmp_path):
     J2 = ptgen.J_from_file(jf)
     w = np.linspace(0.5, 5, 7)
     assert np.allclose(J2(w), QDJ(w), rtol=2e-3)
+
+
+def test_driver_falls_back_when_ace_file_layout_unknown(tmp_path):
+    """An existing `<pt_file>_initial` in a layout the ACE reader does not know (e.g. one ACE itself wrote) is not
+    an error of the call: the driver warns and takes the pqd PT (generated and cached here), as it would with no ACE
+    file present (general_system.py _resolve_pt)"""
+    import warnings
+    from pyaceqd_amd.general_system import general_system as gs
+    from pyaceqd_amd import opgrammar
+    B = opgrammar.to_matrix("1.000*|1><1|_2", 2)
+    kw = dict(dt=0.1, t_mem=0.3, ae=3.0, temperature=4, threshold="9", factor_ah=None, boson_e_max=7, J_file=None,
+              J_to_file=None, use_infinite=True, system_prefix="tls", temp_dir=str(tmp_path) + os.sep, verbose=False)
+    name = str(tmp_path / ptgen.pt_cache_name("tls", 3.0, 4, "9", 0.3, 0.1, use_infinite=True))
+    for suf in ("_initial", "_initial_0", "_repeated", "_repeated_0"):
+        with open(name + suf, "wb") as f:
+            f.write(b"\x00\x01not a layout this reader knows\n")
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        pt = gs._resolve_pt(None, B, **kw)
+    assert any("not in a layout" in str(x.message) for x in w)
+    assert pt.n_init == 6 and os.path.isfile(name + ".npz")
