@@ -265,9 +265,9 @@ int pqd_tl_dynmap_pseudo(pqd_ctx* ctx, const pqd_c128* dm, int32_t n_maps, int32
 int pqd_ptg_qr(void* stream, pqd_c128* W, int32_t m, int32_t n, int32_t pivot, double tol, pqd_c128* Q,
                pqd_c128* R, int32_t* perm, int32_t* rank);
 /* pqd_ptg_jacobi: one-sided Jacobi SVD of a square n x n X (overwritten): X V = U diag(sigma), columns rotated
- * until every pair satisfies |x_p^H x_q| <= tol |x_p| |x_q|. Outputs: X <- U (unit columns, unsorted), V (n x n),
- * sigma (n, unsorted), *sweeps (host). */
-int pqd_ptg_jacobi(void* stream, pqd_c128* X, int32_t n, pqd_c128* V, double* sigma, double tol,
+ * until every pair satisfies |x_p^H x_q| <= tol |x_p| |x_q|; a column with |x_j| < zero_tol ||X||_F is treated as
+ * zero (never rotated). Outputs: X <- U (unit columns, unsorted), V (n x n), sigma (n, unsorted), *sweeps (host). */
+int pqd_ptg_jacobi(void* stream, pqd_c128* X, int32_t n, pqd_c128* V, double* sigma, double tol, double zero_tol,
                    int32_t max_sweeps, int32_t* sweeps);
 
 #ifdef __cplusplus

@@ -123,8 +123,8 @@ _SIGS = {
     # PT generator factorizations on device pointers (ptgen_gpu.py)
     "pqd_ptg_qr": ([C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_double, C.c_void_p, C.c_void_p,
                     C.c_void_p, P_I32], C.c_int),
-    "pqd_ptg_jacobi": ([C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_double, C.c_int32, P_I32],
-                       C.c_int),
+    "pqd_ptg_jacobi": ([C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_double, C.c_double,
+                        C.c_int32, P_I32], C.c_int),
 }
 
 EXPORTED = tuple(_SIGS)

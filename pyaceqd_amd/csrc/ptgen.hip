@@ -370,6 +370,7 @@ struct JacArgs {
     double2* V;   // n x n, accumulated
     int n, nn;    // nn = n rounded up to even (index n is a dummy player)
     double tol;
+    double zero2; // a column with |x|^2 < zero2 is numerically zero: its pairs are never rotated
     int* count;   // rotations in this sweep
 };
 
@@ -389,7 +390,7 @@ __global__ void jac_init_kernel(double2* V, int n) {
 
 // rotate the pair (p, q): [xp xq] J with J = [[cs, sn], [-sn e^{-i phi}, cs e^{-i phi}]], c = xp^H xq = |c| e^{i phi}
 __device__ __forceinline__ bool jac_rotate(double2* xp, double2* xq, double2* vp, double2* vq, int len, int vlen,
-                                           double tol, int lane) {
+                                           double tol, double zero2, int lane) {
     double a = 0.0, b = 0.0;
     double2 c = c_zero();
     for (int r = lane; r < len; r += 64) {
@@ -403,6 +404,10 @@ __device__ __forceinline__ bool jac_rotate(double2* xp, double2* xq, double2* vp
     b = wsum(b);
     c = wsum2(c);
     const double ac = sqrt(c.x * c.x + c.y * c.y);
+    // a column at the rounding floor of the matrix (|x|^2 < zero2) holds no information: rotating it against the
+    // others only shrinks it by eps per pass towards the denormals, where its relative inner products stay noisy
+    // and the sweep would never end (LAPACK's zgesvj skips such columns the same way)
+    if (a < zero2 || b < zero2) return false;
     if (!(ac > tol * sqrt(a * b)) || ac == 0.0) return false;
     const double2 eph = make_double2(c.x / ac, -c.y / ac);  // e^{-i phi}
     const double zeta = (b - a) / (2.0 * ac);
@@ -429,13 +434,13 @@ __global__ __launch_bounds__(256) void jac_round_kernel(JacArgs a, int t) {
     jac_pair(t, i, a.nn, p, q);
     if (q >= a.n) return;
     const bool rot = jac_rotate(a.X + (size_t)p * a.n, a.X + (size_t)q * a.n, a.V + (size_t)p * a.n,
-                                a.V + (size_t)q * a.n, a.n, a.n, a.tol, lane);
+                                a.V + (size_t)q * a.n, a.n, a.n, a.tol, a.zero2, lane);
     if (rot && lane == 0) atomicAdd(a.count, 1);
 }
 
 // single workgroup: X and V in LDS (2 n^2 <= QS_MAX), all sweeps in one launch
 __global__ __launch_bounds__(QS_THREADS) void jac_small_kernel(double2* Xg, double2* Vg, int n, double tol,
-                                                              int max_sweeps, int* sweeps_out) {
+                                                              double zero2, int max_sweeps, int* sweeps_out) {
     extern __shared__ double2 sm[];
     double2* X = sm;
     double2* V = sm + n * n;
@@ -456,7 +461,7 @@ __global__ __launch_bounds__(QS_THREADS) void jac_small_kernel(double2* Xg, doub
                 int p, q;
                 jac_pair(t, i, nn, p, q);
                 if (q >= n) continue;
-                const bool rot = jac_rotate(X + p * n, X + q * n, V + p * n, V + q * n, n, n, tol, lane);
+                const bool rot = jac_rotate(X + p * n, X + q * n, V + p * n, V + q * n, n, n, tol, zero2, lane);
                 if (rot && lane == 0) atomicAdd(&s_cnt, 1);
             }
             __syncthreads();
@@ -538,13 +543,10 @@ hipError_t small_attrs() {
     return hipSuccess;
 }
 
-int g_small_disabled = -1;
+// PQD_PTG_SMALL=0: every factorization on the multi-workgroup kernels (A/B and tests of both paths)
 bool small_ok() {
-    if (g_small_disabled < 0) {
-        const char* e = getenv("PQD_PTG_SMALL");
-        g_small_disabled = (e && atoi(e) == 0) ? 1 : 0;
-    }
-    return !g_small_disabled;
+    const char* e = getenv("PQD_PTG_SMALL");
+    return !(e && atoi(e) == 0);
 }
 
 }  // namespace
@@ -614,7 +616,7 @@ extern "C" int pqd_ptg_qr(void* stream, pqd_c128* Wp, int32_t m, int32_t n, int3
 }
 
 extern "C" int pqd_ptg_jacobi(void* stream, pqd_c128* Xp, int32_t n, pqd_c128* Vp, double* sigma, double tol,
-                              int32_t max_sweeps, int32_t* sweeps_out) {
+                              double zero_tol, int32_t max_sweeps, int32_t* sweeps_out) {
     if (!Xp || !Vp || !sigma || !sweeps_out) return perr(PQD_ERR_ARG, "pqd_ptg_jacobi: NULL argument");
     if (n < 1) return perr(PQD_ERR_ARG, "pqd_ptg_jacobi: empty matrix");
     std::lock_guard<std::mutex> lk(g_mu);
@@ -625,16 +627,25 @@ extern "C" int pqd_ptg_jacobi(void* stream, pqd_c128* Xp, int32_t n, pqd_c128* V
     PCHK(scratch(al(64 * sizeof(int)), &base));
     int* cnt = static_cast<int*>(base);
     int sweeps = 0;
+    // zero threshold relative to the Frobenius norm (rotation-invariant): |x_j| < zero_tol * ||X||_F
+    double fro2 = 0.0;
+    {
+        std::vector<double2> h((size_t)n * n);
+        PCHK(hipMemcpyAsync(h.data(), X, h.size() * sizeof(double2), hipMemcpyDeviceToHost, s));
+        PCHK(hipStreamSynchronize(s));
+        for (const double2& v : h) fro2 += v.x * v.x + v.y * v.y;
+    }
+    const double zero2 = zero_tol * zero_tol * fro2;
     if (small_ok() && 2 * (size_t)n * n <= (size_t)QS_MAX) {
         PCHK(small_attrs());
         hipLaunchKernelGGL(jac_small_kernel, dim3(1), dim3(QS_THREADS), 2 * (size_t)n * n * sizeof(double2), s, X, V,
-                           n, tol, max_sweeps, cnt);
+                           n, tol, zero2, max_sweeps, cnt);
         PCHK(hipGetLastError());
         PCHK(hipMemcpyAsync(&sweeps, cnt, sizeof(int), hipMemcpyDeviceToHost, s));
         PCHK(hipStreamSynchronize(s));
     } else {
         JacArgs a;
-        a.X = X; a.V = V; a.n = n; a.nn = n + (n & 1); a.tol = tol; a.count = cnt;
+        a.X = X; a.V = V; a.n = n; a.nn = n + (n & 1); a.tol = tol; a.zero2 = zero2; a.count = cnt;
         const size_t nv = (size_t)n * n;
         hipLaunchKernelGGL(jac_init_kernel, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, s, V, n);
         const int npair = a.nn / 2, wpb = 4;

@@ -126,7 +126,8 @@ def _resolve_pt(pt_file, boson_mat, *, dt, t_mem, ae, temperature, threshold, fa
                 J_to_file, use_infinite, system_prefix, temp_dir, verbose):
     """The PT for phonons=True (general_system.py:146-211): a ProcessTensor object is used as is; an existing pqd
     PT container (`<pt_file>.npz`, or `pt_file` itself if it is one) is loaded; otherwise the Gaussian-bath PT is
-    generated from the same parameters ACE's generate file holds (pyaceqd_amd.ptgen) and cached under the
+    generated on the GPU from the same parameters ACE's generate file holds (pyaceqd_amd.ptgen_gpu; the host
+    restatement pyaceqd_amd.ptgen with PQD_PTGEN=host) and cached under the
     reference's file name (plus `.npz`) so later calls reuse it, as the reference does with its `_initial` files."""
     if isinstance(pt_file, ProcessTensor):
         return pt_file
@@ -159,9 +160,15 @@ def _resolve_pt(pt_file, boson_mat, *, dt, t_mem, ae, temperature, threshold, fa
     thr = float(threshold) if "e" in str(threshold).lower() or float(threshold) < 1 else 10.0 ** (-float(threshold))
     if verbose:
         print("{} not found. Calculating...".format(pt_file))
-    pt = ptgen.qd_phonon_pt(boson_mat, dt, t_mem=t_mem, ae=ae, temperature=temperature, threshold=thr,
-                            factor_ah=factor_ah, boson_e_max=boson_e_max, J_file=J_file, use_infinite=use_infinite,
-                            verbose=verbose)
+    # generated on the GPU (ptgen_gpu: the same construction with the factorizations in csrc/ptgen.hip);
+    # PQD_PTGEN=host runs the host restatement ptgen.py instead (A/B, and the CPU-only test suite)
+    if os.environ.get("PQD_PTGEN", "gpu") == "host":
+        gen = ptgen.qd_phonon_pt
+    else:
+        from .. import ptgen_gpu
+        gen = ptgen_gpu.qd_phonon_pt_gpu
+    pt = gen(boson_mat, dt, t_mem=t_mem, ae=ae, temperature=temperature, threshold=thr, factor_ah=factor_ah,
+             boson_e_max=boson_e_max, J_file=J_file, use_infinite=use_infinite, verbose=verbose)
     try:
         save_pt(pt_file + ".npz", pt, dim=boson_mat.shape[0])
     except OSError:

@@ -1,0 +1,10 @@
+#!/bin/bash
+set -o pipefail
+mkdir -p gpurun_out/r04
+export PYTHONUNBUFFERED=1
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_ptgen -o ptg -- python3 scripts/bench_ptgen.py --case bx05 --steps 20 > gpurun_out/r04/bench_ptgen_prof.log 2>&1 || { tail -30 gpurun_out/r04/bench_ptgen_prof.log; exit 1; }
+find /tmp/prof_ptgen -name "*stats*" -exec cp {} gpurun_out/r04/ \;
+ls gpurun_out/r04
+timeout -k 10 300 python3 -m cProfile -s tottime scripts/bench_ptgen.py --case bx05 --steps 20 > gpurun_out/r04/cprof_ptgen.log 2>&1 || { tail -30 gpurun_out/r04/cprof_ptgen.log; exit 1; }
+head -60 gpurun_out/r04/cprof_ptgen.log

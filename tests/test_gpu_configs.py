@@ -256,3 +256,36 @@ def test_config5_tomography_scan_chi64_vs_oracle(monkeypatch, tmp_path):
     for (cg, rg), (cr, rr) in zip(got, ref):
         assert np.max(np.abs(rg - rr)) <= 1e-10 * np.max(np.abs(rr))
         assert abs(cg - cr) < 1e-8
+
+
+def test_config5_tomography_scan_chi64_180ps_vs_oracle_subsets(monkeypatch, tmp_path):
+    """C5 at chi = 64 over the class's own (non-regular) t1 grid to tend 180 ps, as C4 is checked: every G2_reuse
+    variant's launch (the whole 2 e0 x 2 bx grid in one multi-system launch, ~7,000 trajectories) is checked on 4 of
+    its trajectories (first, one third, two thirds, last; different grid points) against the C oracle propagating
+    the same trajectories. Tables are downloaded (PQD_SCAN_TRAPZ=0) so the per-trajectory outputs can be compared;
+    the device-trapz path is compared with the table path in test_output_trapz_matches_host_integrals."""
+    from pyaceqd_amd.general_system import general_system as gs
+    from pyaceqd_amd.pol_entanglement.G2 import densitymatrix_reuse_scan
+    monkeypatch.setenv("PQD_SCAN_TRAPZ", "0")
+    real = gs.propagate_table
+    checked = []
+
+    def wrapped(system, grid, rho0, out_ops, traj, pt=None, ctx=None):
+        res = real(system, grid, rho0, out_ops, traj, pt=pt, ctx=ctx)
+        n = traj.n_traj
+        ids = sorted({0, n // 3, (2 * n) // 3, n - 1})
+        sub = _subset(traj, ids)
+        ref = engine.tables_from_outputs(oracle.propagate(system, grid, rho0, out_ops, sub, pt=pt, nthreads=16),
+                                         sub, grid)
+        for k, i in enumerate(ids):
+            assert np.array_equal(res[i][0], ref[k][0])      # the time rows
+            checked.append((n, int(traj.out_end[i]), rel(res[i][1:], ref[k][1:])))
+        return res
+    monkeypatch.setattr(gs, "propagate_table", wrapped)
+    insts, kws = _c5_insts(180.0, tmp_path, t0=62.0, t0b=92.0)
+    got = densitymatrix_reuse_scan(insts, kws, return_rho=True)
+    assert len(got) == 4 and len(insts[0].t1) > 100
+    assert len(checked) == 12, checked                       # 3 variants x 4 trajectories
+    assert all(n > 400 for n, _, _ in checked)               # each launch carries the whole grid
+    assert max(e for _, e, _ in checked) >= 1700             # trajectories run to ~tend
+    assert max(r for _, _, r in checked) < 1e-10, checked

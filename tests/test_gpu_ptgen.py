@@ -1,0 +1,234 @@
+"""GPU PT generator (pyaceqd_amd/ptgen_gpu.py + csrc/ptgen.hip; replaces ACE's `dont_propagate` + `write_PT`,
+reference general_system.py:152-211).
+
+  * the device factorizations against numpy/LAPACK: Householder QR (same reflector convention as zgeqrf, so R
+    equals numpy's R), the rank-revealing column-pivoted QR, and the QR-preconditioned one-sided Jacobi SVD, on
+    both the single-workgroup (LDS) and the multi-workgroup kernels;
+  * the generated PT against the host generator ptgen.py in influence values (path contractions
+    bond0 Q_1[a_1] ... Q_n[a_n] c_n, gauge-invariant) to <= 1e-10, in both tail modes;
+  * the physics pins of tests/test_ptgen.py, now through the GPU generator AND the HIP propagation: the
+    closed-form independent-boson coherence and the exact shift-register PT (oracle/ptgen_oracle.py)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle, ptgen_oracle
+from pyaceqd_amd import engine, ptgen
+from pyaceqd_amd.engine import Grid, System, Trajectories
+from tests import helpers as H
+
+pytestmark = pytest.mark.gpu
+QDJ = lambda w: ptgen.qd_phonon_J(w, ae=3.0)  # noqa: E731
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _dev(a):
+    torch = _torch()
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=torch.complex128, device="cuda")
+
+
+def _rand(rng, m, n, rank=None, scale=None):
+    A = rng.normal(size=(m, n)) + 1j * rng.normal(size=(m, n))
+    if rank is not None:
+        A = (rng.normal(size=(m, rank)) + 1j * rng.normal(size=(m, rank))) @ (
+            rng.normal(size=(rank, n)) + 1j * rng.normal(size=(rank, n)))
+        A += 1e-14 * (rng.normal(size=(m, n)) + 1j * rng.normal(size=(m, n)))
+    if scale is not None:
+        A = A * scale[None, :]
+    return A
+
+
+@pytest.mark.parametrize("small", ["1", "0"])
+@pytest.mark.parametrize("m,n", [(7, 5), (5, 7), (195, 39), (40, 30), (300, 120), (930, 369)])
+def test_ptg_qr_matches_lapack(monkeypatch, small, m, n):
+    from pyaceqd_amd import ptgen_gpu
+    monkeypatch.setenv("PQD_PTG_SMALL", small)
+    rng = np.random.default_rng(m * 1000 + n)
+    W = _rand(rng, m, n)
+    Qc, Rc, perm, k = ptgen_gpu.qr_cols(_dev(W.T))
+    Q, R = Qc.T.cpu().numpy(), Rc.T.cpu().numpy()
+    assert k == min(m, n) and np.array_equal(perm.cpu().numpy(), np.arange(n))
+    assert np.max(np.abs(Q.conj().T @ Q - np.eye(k))) < 1e-13
+    assert np.max(np.abs(Q @ R - W)) < 1e-13 * np.max(np.abs(W)) * np.sqrt(m)
+    assert np.max(np.abs(np.tril(R, -1))) == 0.0
+    Rn = np.linalg.qr(W, mode="r")           # zgeqrf: the same Householder convention, real diagonal
+    assert np.max(np.abs(R - Rn)) < 1e-12 * np.max(np.abs(Rn))
+
+
+@pytest.mark.parametrize("small", ["1", "0"])
+@pytest.mark.parametrize("m,n,rank", [(80, 39, 13), (60, 40, None), (1205, 300, 120), (400, 250, None)])
+def test_ptg_qrcp_rank_revealing(monkeypatch, small, m, n, rank):
+    """column-pivoted QR stopping at a norm tolerance: Q orthonormal, pivots non-increasing, W P = Q R + E with
+    ||E||_F <= sqrt(n - k) tol, and for a numerically rank-r matrix the rank found is r"""
+    from pyaceqd_amd import ptgen_gpu
+    monkeypatch.setenv("PQD_PTG_SMALL", small)
+    rng = np.random.default_rng(m + n)
+    W = _rand(rng, m, n, rank=rank, scale=None if rank else np.logspace(0, -14, n))
+    tol = 1e-10 * np.max(np.linalg.norm(W, axis=0))
+    Qc, Rc, perm, k = ptgen_gpu.qr_cols(_dev(W.T), pivot=True, tol=tol)
+    Q, R, p = Qc.T.cpu().numpy(), Rc.T.cpu().numpy(), perm.cpu().numpy()
+    assert sorted(p) == list(range(n))
+    assert np.max(np.abs(Q.conj().T @ Q - np.eye(k))) < 1e-12
+    E = W[:, p] - Q @ R
+    assert np.linalg.norm(E) <= np.sqrt(n - k + 1) * tol * 1.01 + 1e-13 * np.linalg.norm(W)
+    d = np.abs(np.diag(R[:, :k]))
+    assert np.all(d[1:] <= d[:-1] * (1 + 1e-12))
+    if rank is not None:
+        assert k == rank
+
+
+@pytest.mark.parametrize("small", ["1", "0"])
+@pytest.mark.parametrize("r,c,graded", [(6, 9, False), (40, 200, True), (384, 1350, False), (300, 90, True),
+                                         (120, 120, True), (45, 101, "lowrank"), (201, 700, "lowrank")])
+def test_ptg_svd_matches_lapack(monkeypatch, small, r, c, graded):
+    """thin SVD vs LAPACK on random, graded (1 .. 1e-13) and numerically low-rank blocks (odd sizes: the Jacobi
+    tournament's dummy player; rank 1/4: three quarters of the columns at the rounding floor, as the stacked
+    generator blocks are)"""
+    from pyaceqd_amd import ptgen_gpu
+    monkeypatch.setenv("PQD_PTG_SMALL", small)
+    rng = np.random.default_rng(r * 7 + c)
+    k = min(r, c)
+    if graded == "lowrank":
+        A = _rand(rng, r, c, rank=k // 4)
+    elif graded:
+        U0 = np.linalg.qr(_rand(rng, r, k))[0]
+        V0 = np.linalg.qr(_rand(rng, c, k))[0]
+        A = (U0 * np.logspace(0, -13, k)[None, :]) @ V0.conj().T
+    else:
+        A = _rand(rng, r, c)
+    U, S, Vh = (x.cpu().numpy() for x in ptgen_gpu.svd(_dev(A)))
+    Sn = np.linalg.svd(A, compute_uv=False)
+    kk = len(S)                                    # the numerical rank at 1e-14 (the rest is dropped)
+    assert np.max(np.abs(S - Sn[:kk])) < 1e-13 * Sn[0]
+    assert np.all(Sn[kk:] < 1e-12 * Sn[0])
+    assert np.all(np.diff(S) <= 0)
+    # singular vectors of the numerical rank (the null space of a rank-deficient block is arbitrary: its columns sit at
+    # the rounding floor and are never rotated, and the generator truncates them away)
+    kr = min(kk, int(np.count_nonzero(Sn > 1e-13 * Sn[0])))
+    assert np.max(np.abs(U[:, :kr].conj().T @ U[:, :kr] - np.eye(kr))) < 1e-12
+    assert np.max(np.abs(Vh[:kr] @ Vh[:kr].conj().T - np.eye(kr))) < 1e-12
+    assert np.max(np.abs((U * S[None, :]) @ Vh - A)) < 1e-13 * Sn[0] * np.sqrt(max(r, c))
+
+
+# ---------------------------------------------------------------------------------------------------- the PT
+def influence(pt, paths):
+    """bond0 Q_s(1)[g(a_1)] ... Q_s(n)[g(a_n)] c_s(n) for each path of Liouville indices (the slice schedule of
+    engine semantics: slice n for n < n_init, then the repeated slices)"""
+    out = []
+    for path in paths:
+        v = pt.bond0.copy()
+        s = 0
+        for n, a in enumerate(path):
+            s = n if n < pt.n_init else pt.n_init + (n - pt.n_init) % (pt.n_slices - pt.n_init)
+            v = v @ pt.Q[s, pt.gmap[a]]
+        out.append(v @ pt.closure[s])
+    return np.array(out)
+
+
+@pytest.mark.parametrize("tail", ["svd", "qrcp"])
+@pytest.mark.parametrize("lam,K,T,mb", [([0, 1, 1, 2], 4, 4.0, 0), ([0, 1], 5, 4.0, 0), ([0, 1, 1, 2, 2, 3], 3, 1.0, 0),
+                                        ([0, 1, 1, 2], 6, 4.0, 32)])
+def test_gpu_generator_matches_host_influence(tail, lam, K, T, mb):
+    """GPU generator vs ptgen.py (the host restatement) on the same parameters: influence values of 400 random
+    paths spanning the explicit and the repeated slices agree to 1e-10 (threshold 1e-11; bond uncapped (chi 54-132),
+    and capped at 32 where the cap, not the threshold, decides the slice: the same top-32 subspace)"""
+    from pyaceqd_amd import ptgen_gpu
+    A = np.diag(np.array(lam, dtype=float))
+    eta, delta = ptgen.eta_coefficients(QDJ, T, 0.1, K)
+    ph = ptgen.build_gaussian_pt(A, 0.1, eta, delta, threshold=1e-11, max_bond=mb)
+    pg = ptgen_gpu.build_gaussian_pt_gpu(A, 0.1, eta, delta, threshold=1e-11, max_bond=mb, tail=tail)
+    assert pg.n_init == ph.n_init == 2 * K and pg.n_slices == ph.n_slices
+    rng = np.random.default_rng(K + len(lam))
+    N2 = len(lam) ** 2
+    paths = [rng.integers(0, N2, size=rng.integers(1, 3 * K + 4)) for _ in range(400)]
+    a, b = influence(pg, paths), influence(ph, paths)
+    assert np.max(np.abs(a - b)) < 1e-10 * np.max(np.abs(b))
+    assert np.max(np.abs(b)) > 0.1
+
+
+@pytest.mark.parametrize("lam,K,n_init", [([0, 1], 3, 9), ([0, 1, 1], 2, 4), ([0, 1, 1, 2], 2, 7), ([0, 2], 1, 2)])
+def test_gpu_generator_exact_shift_register_on_hip(lam, K, n_init):
+    """test_ptgen.py's shift-register pin through the GPU generator, propagated on the HIP sweep: driven, damped
+    N-level system, 30x bath, threshold 1e-14, 40 steps vs the exact uncompressed PT (oracle/ptgen_oracle.py)"""
+    from pyaceqd_amd import ptgen_gpu
+    N = len(lam)
+    A = np.diag(np.array(lam, dtype=float))
+    J = lambda w: 30 * QDJ(w)  # noqa: E731
+    eta, delta = ptgen.eta_coefficients(J, 4.0, 0.1, K)
+    sysd, grid = H.random_system(N, n_steps=40, seed=3 + N)
+    rho0 = H.random_rho(N)
+    ops = [H.ketbra(N, i, j) for i in range(N) for j in range(N)]
+    tr = Trajectories(np.array([0, 5]), np.array([40, 33]))
+    pg = ptgen_gpu.build_gaussian_pt_gpu(A, 0.1, eta, delta, threshold=1e-14, max_bond=0, n_init=n_init)
+    pe = ptgen_oracle.exact_if_pt(A, eta, delta, 0.1)
+    got = engine.propagate(sysd, grid, rho0, ops, tr, pt=pg)
+    ref = oracle.propagate(sysd, grid, rho0, ops, tr, pt=pe)
+    bare = oracle.propagate(sysd, grid, rho0, ops, tr)
+    for a, b, c in zip(got, ref, bare):
+        assert np.max(np.abs(a - b)) < 1e-11
+        assert np.max(np.abs(b - c)) > 1e-2
+
+
+@pytest.mark.parametrize("K,thr", [(4, 1e-10), (5, 1e-11)])
+def test_gpu_generator_ibm_on_hip(K, thr):
+    """undriven pure dephasing of a TLS with QD phonons at 4 K (8K steps: explicit, then repeated slices) through
+    the GPU generator AND the HIP sweep vs the discretised independent-boson coherence: <= 1e-6 relative at every
+    step (the north star's phonon tolerance; the host generator reaches 4e-9 / 5e-10 here, chi 49 / 110), trace
+    preserved"""
+    from pyaceqd_amd import ptgen_gpu
+    dt = 0.1
+    eta, delta = ptgen.eta_coefficients(QDJ, 4.0, dt, K)
+    pt = ptgen_gpu.build_gaussian_pt_gpu(np.diag([0.0, 1.0]), dt, eta, delta, threshold=thr, max_bond=0)
+    assert pt.chi <= 128
+    n = 8 * K
+    out = engine.propagate(System(dim=2, H0=np.zeros((2, 2))), Grid(0.0, dt, n), 0.5 * np.ones((2, 2), complex),
+                           [H.ketbra(2, 0, 1), np.eye(2)], Trajectories(np.array([0]), np.array([n])), pt=pt)[0]
+    ex = ptgen_oracle.ibm_coherence_discrete(eta, delta, dt, n)
+    assert np.max(np.abs(out[:, 0] - ex) / np.abs(ex)) < 1e-6
+    assert np.max(np.abs(out[:, 1] - 1)) < 1e-9
+
+
+def test_driver_generates_on_the_gpu(tmp_path, monkeypatch):
+    """system_ace_stream(phonons=True) without a PT file generates the PT on the GPU by default; the cached PT has
+    the host generator's influence values (PQD_PTGEN=host)"""
+    from pyaceqd_amd.general_system import general_system as gs
+    from pyaceqd_amd import opgrammar
+    B = opgrammar.to_matrix("1*(|1><1|_4 + |2><2|_4) + 2*|3><3|_4", 4)
+    kw = dict(dt=0.1, t_mem=0.4, ae=3.0, temperature=4, threshold="11", factor_ah=None, boson_e_max=7, J_file=None,
+              J_to_file=None, use_infinite=False, system_prefix="bx", temp_dir=str(tmp_path) + os.sep, verbose=False)
+    called = []
+    from pyaceqd_amd import ptgen_gpu
+    real = ptgen_gpu.qd_phonon_pt_gpu
+    monkeypatch.setattr(ptgen_gpu, "qd_phonon_pt_gpu", lambda *a, **k: called.append(1) or real(*a, **k))
+    pg = gs._resolve_pt(None, B, **kw)
+    assert called
+    monkeypatch.setenv("PQD_PTGEN", "host")
+    ph = gs._resolve_pt(None, B, **dict(kw, temp_dir=str(tmp_path / "h") + os.sep))
+    rng = np.random.default_rng(1)
+    paths = [rng.integers(0, 16, size=rng.integers(1, 14)) for _ in range(200)]
+    a, b = influence(pg, paths), influence(ph, paths)
+    assert np.max(np.abs(a - b)) < 1e-10 * np.max(np.abs(b))
+
+
+def test_gpu_generator_biexciton_reference_default_timed():
+    """the biexciton PT at the reference's own defaults (four_level_system/linear.py:8: dt 0.5, t_mem 20.48 ->
+    K = 41, T 4 K, threshold 1e-10, bond cap 128): generated on the GPU in well under a minute, slices bounded,
+    trace preserving (closure of the trace path = 1 for every step of a free run)"""
+    import time
+    from pyaceqd_amd import ptgen_gpu
+    t0 = time.perf_counter()
+    pt = ptgen_gpu.qd_phonon_pt_gpu(np.diag([0.0, 1.0, 1.0, 2.0]), 0.5, t_mem=20.48, ae=3.0, temperature=4,
+                                    threshold=1e-10)
+    el = time.perf_counter() - t0
+    print(f"biexciton K=41 PT on the GPU: {el:.1f} s, chi {pt.chi}, slices {pt.n_slices}")
+    assert pt.n_init == 82 and pt.chi <= 128
+    assert el < 60.0
+    # the path that stays on |0><0| (coupling eigenvalue 0 on both sides) has influence exactly 1; the PT keeps it to
+    # its truncation error (the bond cap of 128 binds here; measured 1.2e-7 after 120 steps)
+    inf = influence(pt, [np.zeros(n, dtype=int) for n in (1, 10, 82, 120)])
+    assert np.max(np.abs(inf - 1)) < 1e-6

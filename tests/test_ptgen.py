@@ -94,9 +94,12 @@ def test_bond_cap_and_padding():
     assert pt.D == 4 and list(pt.gmap) == [0, 1, 2, 3]
 
 
-def test_driver_generates_and_caches_pt(tmp_path):
+def test_driver_generates_and_caches_pt(tmp_path, monkeypatch):
     """system_ace_stream(phonons=True) without a PT file: generate from the ACE generate-file parameters, cache
-    under the reference's name (+ .npz), reuse on the next call; J_to_file writes J(omega)"""
+    under the reference's name (+ .npz), reuse on the next call; J_to_file writes J(omega). (The driver generates on
+    the GPU by default; this CPU test takes the host restatement, PQD_PTGEN=host: tests/test_gpu_ptgen.py runs the
+    default.)"""
+    monkeypatch.setenv("PQD_PTGEN", "host")
     from pyaceqd_amd.general_system import general_system as gs
     from pyaceqd_amd import opgrammar
     B = opgrammar.to_matrix("1.000*|1><1|_2", 2)
@@ -118,11 +121,12 @@ def test_driver_generates_and_caches_pt(tmp_path):
     assert np.allclose(J2(w), QDJ(w), rtol=2e-3)
 
 
-def test_driver_falls_back_when_ace_file_layout_unknown(tmp_path):
+def test_driver_falls_back_when_ace_file_layout_unknown(tmp_path, monkeypatch):
     """An existing `<pt_file>_initial` in a layout the ACE reader does not know (e.g. one ACE itself wrote) is not
     an error of the call: the driver warns and takes the pqd PT (generated and cached here), as it would with no ACE
     file present (general_system.py _resolve_pt)"""
     import warnings
+    monkeypatch.setenv("PQD_PTGEN", "host")
     from pyaceqd_amd.general_system import general_system as gs
     from pyaceqd_amd import opgrammar
     B = opgrammar.to_matrix("1.000*|1><1|_2", 2)
