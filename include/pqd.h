@@ -245,6 +245,13 @@ int pqd_dynamics_t1(pqd_ctx* ctx, const pqd_c128* dm_1, const pqd_c128* dm_2, co
                     const double* t1, const pqd_c128* precalc, int32_t n_t, double dt, int32_t n_map,
                     int32_t dim, double tb, int32_t n_precalc, pqd_c128* result);
 
+/* ---- tau tails on one constant map (the `for j: X = tl_map2 @ X; G[:, n_tauc + j + 1] = Bt @ X` loops of
+ * tl_three_op_two_time_phonons / tl_threeoptwotime_phonons_dm, reference two_time/correlations.py:866-1186) ----
+ * out[i][j] = w . M^{j+1} x_i for i < n_x, j < n_steps. M: N2 x N2 row-major, X: [n_x][N2] row-major, w: N2,
+ * out: [n_x][n_steps] row-major. N2 in {4, 9, 16, 25, 36}. */
+int pqd_map_tail(pqd_ctx* ctx, const pqd_c128* M, int32_t N2, const pqd_c128* X, int32_t n_x, const pqd_c128* w,
+                 int32_t n_steps, pqd_c128* out);
+
 /* ---- time-local dynamical maps (replaces tools.calc_tl_dynmap_pseudo, reference tools.py:446-484) ----
  * dm: n_maps row-major n x n maps, dm[i] = E(t_{i+1}, t0). out (n_maps maps): out[0] = dm[0],
  * out[i] = dm[i] pinv(dm[i-1]) with singular values <= rcond * max(s) dropped (numpy pinv, rcond

@@ -265,6 +265,17 @@ def dynamics_t1(dm_1, dm_2, rho_init, t1, precalc, dt, dim, tb):
     return out
 
 
+def map_tail(M, X, w, n_steps):
+    """checker for pqd_map_tail: the reference's own loop (two_time/correlations.py:866-1011, `for j: X = tl_map2 @ X;
+    G[:, n_tauc + j + 1] = Bt @ X`), X with one column per row. Returns (n_x, n_steps)."""
+    X = np.array(X, dtype=np.complex128, copy=True)
+    out = np.zeros((X.shape[1], max(0, int(n_steps))), dtype=np.complex128)
+    for j in range(int(n_steps)):
+        X = M @ X
+        out[:, j] = w @ X
+    return out
+
+
 def tl_dynmap_pseudo(dm, n_out=None, rcond=1e-12):
     """time-local maps out[i] = dm[i] pinv(dm[i-1], rcond), out[0] = dm[0] — numpy restatement of
     calc_tl_dynmap_pseudo (reference pyaceqd/tools.py:446-484, LAPACK SVD inside numpy's pinv)"""

@@ -120,6 +120,7 @@ _SIGS = {
     "pqd_dynamics_t1": ([C.c_void_p, P_C128, P_C128, P_C128, P_F64, P_C128, C.c_int32, C.c_double, C.c_int32,
                          C.c_int32, C.c_double, C.c_int32, P_C128], C.c_int),
     "pqd_tl_dynmap_pseudo": ([C.c_void_p, P_C128, C.c_int32, C.c_int32, C.c_double, P_C128], C.c_int),
+    "pqd_map_tail": ([C.c_void_p, P_C128, C.c_int32, P_C128, C.c_int32, P_C128, C.c_int32, P_C128], C.c_int),
     # PT generator factorizations on device pointers (ptgen_gpu.py)
     "pqd_ptg_qr": ([C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_double, C.c_void_p, C.c_void_p,
                     C.c_void_p, P_I32], C.c_int),

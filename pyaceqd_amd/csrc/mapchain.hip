@@ -513,6 +513,50 @@ __global__ __launch_bounds__(64) void propagate_tau_kernel(const double2* dm, co
 }
 
 // ---------------------------------------------------------------------------------------------
+// tau tails of the phonon dynamical-map correlations (reference two_time/correlations.py:866-1186:
+// `for j: X = tl_map2 @ X; G[:, n_tauc + j + 1] = Bt @ X`): every row's vector x_i is propagated by ONE constant
+// map, out[i][j] = w . M^{j+1} x_i. Rows are independent: 64 / N2 rows packed per wave (lane = row r of M, held in
+// registers), the vector double-buffered in LDS, the trace w . y summed by lane 0 of the row's lanes.
+// ---------------------------------------------------------------------------------------------
+template <int N2>
+__global__ __launch_bounds__(64) void map_tail_kernel(const double2* __restrict__ M, const double2* __restrict__ X,
+                                                      int n_x, const double2* __restrict__ w, int n_steps,
+                                                      double2* __restrict__ out) {
+    constexpr int TPW = 64 / N2;
+    __shared__ double2 xs[2][64], ts[64];
+    const int lane = threadIdx.x;
+    const int tl = lane / N2, r = lane - (lane / N2) * N2;
+    const int i = blockIdx.x * TPW + tl;
+    const bool act = tl < TPW && i < n_x;
+    double2 mrow[N2];
+#pragma unroll
+    for (int c = 0; c < N2; ++c) mrow[c] = act ? M[(size_t)r * N2 + c] : c_zero();
+    const double2 wr = act ? w[r] : c_zero();
+    xs[0][lane] = act ? X[(size_t)i * N2 + r] : c_zero();
+    const int tlx = tl < TPW ? tl : 0;
+    __syncthreads();
+    int cur = 0;
+    for (int j = 0; j < n_steps; ++j) {
+        const double2* x = xs[cur] + tlx * N2;
+        double2 y = c_zero();
+#pragma unroll
+        for (int c = 0; c < N2; ++c) c_fma(y, mrow[c], x[c]);
+        xs[cur ^ 1][lane] = y;
+        ts[lane] = c_mul(wr, y);
+        __syncthreads();
+        if (act && r == 0) {
+            double2 s = c_zero();
+#pragma unroll
+            for (int q = 0; q < N2; ++q) s = c_add(s, ts[tl * N2 + q]);
+            out[(size_t)i * n_steps + j] = s;
+        }
+        cur ^= 1;
+        __syncthreads();
+    }
+}
+
+
+// ---------------------------------------------------------------------------------------------
 // timebin_tl.f90: propagate_tb with uniform control flow across the packed pairs of a wave
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ double round6(double x) { return (double)llround(x * 1000000.0) / 1000000.0; }
@@ -727,6 +771,21 @@ hipError_t launch_mapchain_blocked(const MapChainParams& p, int n_chain, hipStre
         case 36: return launch_blocked_n<36, 1>(p, n_chain, s);
         default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_map_tail(int N2, const double2* M, const double2* X, int n_x, const double2* w, int n_steps,
+                           double2* out, hipStream_t s) {
+    const int TPW = 64 / N2;
+    const dim3 grid((n_x + TPW - 1) / TPW);
+    switch (N2) {
+        case 4: hipLaunchKernelGGL(map_tail_kernel<4>, grid, dim3(64), 0, s, M, X, n_x, w, n_steps, out); break;
+        case 9: hipLaunchKernelGGL(map_tail_kernel<9>, grid, dim3(64), 0, s, M, X, n_x, w, n_steps, out); break;
+        case 16: hipLaunchKernelGGL(map_tail_kernel<16>, grid, dim3(64), 0, s, M, X, n_x, w, n_steps, out); break;
+        case 25: hipLaunchKernelGGL(map_tail_kernel<25>, grid, dim3(64), 0, s, M, X, n_x, w, n_steps, out); break;
+        case 36: hipLaunchKernelGGL(map_tail_kernel<36>, grid, dim3(64), 0, s, M, X, n_x, w, n_steps, out); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_propagate_tau(int N2, const double2* dm, const double2* rho0, int n_tau, int j_start,

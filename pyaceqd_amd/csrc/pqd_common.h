@@ -224,6 +224,8 @@ hipError_t launch_four_time(const FourTimeParams& p, hipStream_t s);
 hipError_t launch_propagate_tau(int N2, const double2* dm, const double2* rho0, int n_tau, int j_start,
                                 double2* out, hipStream_t s);
 hipError_t launch_dynamics_t1(const FourTimeParams& p, double2* out, hipStream_t s);
+hipError_t launch_map_tail(int N2, const double2* M, const double2* X, int n_x, const double2* w, int n_steps,
+                           double2* out, hipStream_t s);
 hipError_t launch_tl_dynmap(const double2* dm, int n_maps, int n, double rcond, double2* out, hipStream_t s);
 int tl_dynmap_nmax();
 bool split_supported(int N2, int CHI, int n_traj, int n_cu);

@@ -1543,6 +1543,25 @@ int pqd_propagate_tau(pqd_ctx* ctx, const pqd_c128* dm_tl, int32_t n_maps, const
     return PQD_OK;
 }
 
+int pqd_map_tail(pqd_ctx* ctx, const pqd_c128* M, int32_t N2, const pqd_c128* X, int32_t n_x, const pqd_c128* w,
+                 int32_t n_steps, pqd_c128* out) {
+    if (!ctx || !M || !X || !w || !out) return fail(PQD_ERR_ARG, "NULL argument");
+    if (!(N2 == 4 || N2 == 9 || N2 == 16 || N2 == 25 || N2 == 36)) return fail(PQD_ERR_UNSUPPORTED, "N2 %d", N2);
+    if (n_x < 0 || n_steps < 0) return fail(PQD_ERR_ARG, "n_x %d n_steps %d", n_x, n_steps);
+    if (n_x == 0 || n_steps == 0) return PQD_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    DevBuf<double2> dM, dX, dw, o;
+    HIPCHK(dM.upload(reinterpret_cast<const double2*>(M), (size_t)N2 * N2, s));
+    HIPCHK(dX.upload(reinterpret_cast<const double2*>(X), (size_t)n_x * N2, s));
+    HIPCHK(dw.upload(reinterpret_cast<const double2*>(w), N2, s));
+    HIPCHK(o.alloc((size_t)n_x * n_steps));
+    HIPCHK(launch_map_tail(N2, dM.p, dX.p, n_x, dw.p, n_steps, o.p, s));
+    HIPCHK(hipMemcpyAsync(out, o.p, (size_t)n_x * n_steps * sizeof(double2), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return PQD_OK;
+}
+
 static int four_time_common(pqd_ctx* ctx, FourTimeParams& p, const pqd_c128* dm_1, const pqd_c128* dm_2,
                             const pqd_c128* rho_init, const double* t1, const pqd_c128* precalc, const pqd_c128* ops,
                             int n_ops, pqd_c128* result, bool dyn, int row_lo = 0, int row_hi = INT_MAX) {

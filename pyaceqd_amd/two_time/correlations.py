@@ -293,10 +293,10 @@ def tl_three_op_two_time_phonons(system, t_axis, *pulses, t_mem=10, opA="|1><0|_
             rho_t = blk[j] @ rho_t
             G[i, j + 1] = Bt @ rho_t
         X[:, i] = rho_t
-    rows = np.arange(len(t_axis))
-    for j in range(n_tau - n_tauc):
-        X = tl_map2 @ X
-        G[rows, n_tauc + j + 1] = Bt @ X
+    # the tails past the memory block, every row on the last time-local map, on the GPU (pqd_map_tail)
+    n_tail = n_tau - n_tauc
+    if n_tail > 0:
+        G[:, n_tauc + 1: n_tauc + 1 + n_tail] = propagate_tau_module.map_tail(tl_map2, X, Bt, n_tail)
     return t_axis, tau, G
 
 
@@ -357,9 +357,9 @@ def tl_threeoptwotime_phonons_dm(system, t_axis, *pulses, t_mem=10, opA="|1><0|_
 
 
 def _tail_rows(G, i, x, tl_map2, col0, n, Bt):
-    for j in range(n):
-        x = tl_map2 @ x
-        G[i, col0 + j + 1] = Bt @ x
+    """G[i, col0 + 1 + j] = Bt . tl_map2^{j+1} x on the GPU (pqd_map_tail)"""
+    if n > 0:
+        G[i, col0 + 1: col0 + 1 + n] = propagate_tau_module.map_tail(tl_map2, np.asarray(x)[:, None], Bt, n)[0]
 
 
 def _tl_stationary_three_op(system, t_axis, pulses, t_mem, ops, tau_max, dt, rho0, options, mtos_dyn):

@@ -34,6 +34,24 @@ def propagate_tau(dm_tl, rho_init, n_tau, dim, j_start):
     return out
 
 
+def map_tail(M, X, w, n_steps):
+    """G[i, j] = w . M^{j+1} x_i (i < n_x = X.shape[1], j < n_steps) on the GPU (pqd_map_tail): the tau tails of the
+    phonon dynamical-map correlations (correlations.py:866-1186: `X = tl_map2 @ X; G[:, n_tauc + j + 1] = Bt @ X`),
+    X with one column per row i (the reference's layout). Returns (n_x, n_steps) complex."""
+    M = np.ascontiguousarray(M, dtype=np.complex128)
+    Xr = np.ascontiguousarray(np.asarray(X, dtype=np.complex128).T)        # [n_x][N2]
+    w = np.ascontiguousarray(w, dtype=np.complex128)
+    n_x, N2 = Xr.shape
+    out = np.zeros((n_x, max(0, int(n_steps))), dtype=np.complex128)
+    if n_x == 0 or n_steps <= 0:
+        return out
+    ctx = _ctx()
+    with ctx.lock:
+        _lib.check(_lib.lib().pqd_map_tail(ctx.handle, _lib.cptr(M), int(N2), _lib.cptr(Xr), int(n_x), _lib.cptr(w),
+                                           int(n_steps), _lib.cptr(out)))
+    return out
+
+
 def calc_onetime_parallel(dm_tl, rho_init, n_tau, dim, opa, opb, opc, time, time_sparse, n_t=None, n_tfull=None):
     """G(t_i, tau_k) on the dynamical-map chain (propagate_tau.f90:110-187)"""
     dm_tl, rho_init = _c(dm_tl), _c(rho_init)

@@ -51,13 +51,14 @@ def _opts(**k):
 
 
 def _oracle_kernels(monkeypatch):
-    """CPU stand-ins for the two GPU kernels of the map paths (test infrastructure only)"""
+    """CPU stand-ins for the GPU kernels of the map paths (test infrastructure only)"""
     from oracle import oracle
     from pyaceqd_amd.two_time import propagate_tau_module as ptm
     monkeypatch.setattr(corr, "calc_tl_dynmap_pseudo", lambda dm, t, debug=False: oracle.tl_dynmap_pseudo(
         np.asarray(dm)[: len(t) - 1]))
     monkeypatch.setattr(ptm, "calc_onetime_parallel", lambda dm, r, n_tau, dim, a, b, c, t, ts: oracle.
                         calc_onetime_parallel(dm, r, n_tau, dim, a, b, c, np.real(t), ts))
+    monkeypatch.setattr(ptm, "map_tail", oracle.map_tail)
 
 
 def _oracle_propagation(monkeypatch):

@@ -423,6 +423,22 @@ def test_mapchain_blocked_sweep_block_mode_vs_oracle(monkeypatch, dim, L, n_map)
     assert rel(a, c) < 1e-11
 
 
+@pytest.mark.parametrize("dim", [2, 3, 4, 5, 6])
+def test_map_tail_vs_oracle(dim):
+    """pqd_map_tail (the tau tails of the phonon dynamical-map correlations, correlations.py:866-1186) vs the
+    reference loop restated in oracle.map_tail: 37 rows (ragged against the rows packed per wave), 1,500 steps"""
+    from pyaceqd_amd.two_time import propagate_tau_module as M
+    rng = np.random.default_rng(70 + dim)
+    N2 = dim * dim
+    Mm = np.eye(N2) + 0.05 * (rng.normal(size=(N2, N2)) + 1j * rng.normal(size=(N2, N2))) / dim
+    X = rng.normal(size=(N2, 37)) + 1j * rng.normal(size=(N2, 37))
+    w = rng.normal(size=N2) + 1j * rng.normal(size=N2)
+    a = M.map_tail(Mm, X, w, 1500)
+    b = oracle.map_tail(Mm, X, w, 1500)
+    assert a.shape == (37, 1500)
+    assert rel(a, b) < 1e-12
+
+
 def test_mapchain_blocked_refuses_reads_past_the_maps():
     """a tau window running past the last map is refused (the Fortran would read past dm_tl)"""
     from pyaceqd_amd.two_time import propagate_tau_module as M
