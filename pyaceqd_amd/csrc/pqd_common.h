@@ -100,7 +100,7 @@ struct SweepParams {
     int umax;                //   a unit with slice < 0 ends a wave's list; NULL: rows a = wave + k BT
     int trpre;               // 1: traces one lane per (trajectory, output, row), W rows fetched a step ahead
     int ablate;              // diagnostics only (PQD_ABLATE): 1 skip PT, 2 skip column phases, 4 skip outputs
-    int split_b128;          // split groups: 16-B sc1 exchange accesses (A/B switch, PQD_SPLIT_B128 at plan creation)
+    int split_gran;          // split groups: data-tagged granule exchange (default 1; PQD_SPLIT_GRAN=0: counter form)
     unsigned* flags;         // bit 0: a non-finite output value (set by launch_check_finite at synchronize)
     unsigned spin_limit;     // split groups: polls before a wait for the peers times out (PQD_SPLIT_SPIN, tests)
     int traj_base;           // split groups: trajectory of group 0 (a batch run as several co-resident launches)

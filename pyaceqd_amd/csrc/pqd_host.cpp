@@ -611,7 +611,7 @@ static int plan_trunks(pqd_plan* P, pqd_ctx* ctx, int n_sys, const std::vector<s
     P->tk_split = mode != 0 && N2 >= 9 && bpc >= 1 && fit >= 1 &&
                   split_supported(N2, CHI, std::min(nt, fit), n_cu * bpc) &&
                   nt <= (N2 >= 25 ? 4 : 2) * fit;  // launches in a row still beat one batched pass (§4.6 latencies)
-    HIPCHK(P->tk_Xs.alloc((size_t)nt * 2 * N2 * CHI));
+    HIPCHK(P->tk_Xs.alloc((size_t)nt * 4 * N2 * CHI));  // split exchange: 2 slots of granules (pt_split.hip)
     HIPCHK(P->tk_cnt.alloc((size_t)nt * 32));
     HIPCHK(P->tk_err.alloc(4));
     (void)ctx;
@@ -1025,7 +1025,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     sp.blk_act = P->blk_act.p; sp.blk_src = P->blk_src.p;
     sp.traj_sys = P->traj_sys.p; sp.m_stride = (long long)2 * ns * m2; sp.wbeg = P->wbeg.p; sp.wend = P->wend.p;
     { const char* ab = getenv("PQD_ABLATE"); sp.ablate = ab ? atoi(ab) : 0; }
-    { const char* b1 = getenv("PQD_SPLIT_B128"); sp.split_b128 = (b1 && atoi(b1) != 0) ? 1 : 0; }
+    { const char* b1 = getenv("PQD_SPLIT_GRAN"); sp.split_gran = (b1 && atoi(b1) == 0) ? 0 : 1; }
     // polls of a split group's counter before the wait counts as a timeout (~0.1 s); PQD_SPLIT_SPIN overrides
     // it (tests provoke the batched fallback with 0)
     { const char* sl = getenv("PQD_SPLIT_SPIN"); sp.spin_limit = sl ? (unsigned)strtoul(sl, nullptr, 10) : (1u << 22); }
@@ -1076,7 +1076,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     if (const char* e = getenv("PQD_QPRIO")) sp.qprio = atoi(e) & 3;
     finalize_trunks(P);
     if (P->split) {
-        HIPCHK(P->Xs.alloc((size_t)P->n_traj * 2 * N2 * P->CHI));
+        HIPCHK(P->Xs.alloc((size_t)P->n_traj * 4 * N2 * P->CHI));  // split exchange: 2 slots of granules
         HIPCHK(P->cnt.alloc((size_t)P->n_traj * 32));
         HIPCHK(P->err.alloc(4));
     }

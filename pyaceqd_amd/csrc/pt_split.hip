@@ -8,15 +8,20 @@
 // column phases (M_b(n-1), MTOs, outputs, M_a(n), or the fused F(n) = M_a(n) M_b(n-1)) mix rows, so
 // every workgroup gathers the whole state (N2 x chi, 16 KiB at C3) once per step and runs them
 // redundantly — ONE exchange per step instead of a row/column transpose pair.
-// Hand-off (MI355X_MICROARCH.md § visibility, "Valid forms", table row 1): every payload store is
-// an 8-B relaxed agent-scope atomic (global_store sc1), every storing wave drains with
-// s_waitcnt vmcnt(0), a workgroup barrier, then ONE lane adds to the group's monotonic counter
-// (agent-scope atomic); wave 0 polls it with relaxed agent-scope loads (global_load sc1), the other
-// waves wait at a barrier, and every load of the payload is such an sc1 load — so no fences. The
-// exchange buffer is double-buffered by step parity (a workgroup cannot publish step n+2 before
-// every peer has gathered step n). One workgroup per CU (the LDS request forces it) and at most
-// n_cu workgroups (host check), so every workgroup is resident; every spin is bounded and a
-// timeout ends the kernel with an error word the host turns into PQD_ERR_HIP.
+// Hand-off (round 4, default): data-tagged granules (cdna_hip_programming.md §6 Guideline 16 R2: "the data
+// IS the flag"). Every 32-bit word of the row a workgroup publishes travels as one naturally aligned 8-B
+// {tag = step + 1, word} granule written by ONE relaxed agent-scope atomic store (global_store_dwordx2 sc1);
+// the consumers sweep the whole state's granules with sc1 loads and re-read the ones whose tag is not yet
+// the step's, until every tag matches. No drain, no counter, no barrier between publishing and reading: the
+// round-3 form below cost a drain + counter add + poll + 16 KiB gather per step (C3 single run 5.6 us/step).
+// Round-3 form (PQD_SPLIT_GRAN=0, MI355X_MICROARCH.md § visibility "Valid forms" table row 1): payload stores
+// 8-B sc1 atomics, every storing wave drains with s_waitcnt vmcnt(0), a workgroup barrier, then ONE lane adds
+// to the group's monotonic counter; wave 0 polls it with relaxed sc1 loads, the other waves wait at a barrier,
+// and every payload load is an sc1 load — so no fences.
+// Either exchange buffer is double-buffered by step parity (a workgroup cannot publish step n+2 before every
+// peer has gathered step n: its step n+1 row depends on that gather). One workgroup per CU (the LDS request
+// forces it) and at most n_cu workgroups (host check), so every workgroup is resident; every spin is bounded
+// and a timeout ends the kernel with an error word the host turns into PQD_ERR_HIP (then the batched kernel).
 // Semantics are the sweep's: step n applies M_b(n-1), applyBefore MTOs at n,
 // output(n), applyAfter MTOs at n, M_a(n), PT(n); steps without MTOs use F(n) and read the outputs
 // through W(n) = ovec M_b(n-1), as the batched kernel does.
@@ -47,15 +52,9 @@ __device__ __forceinline__ double2 gld(const double2* p) {
 
 typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
 
-// 16-B sc1 payload accesses through a buffer descriptor (aux 16 = sc1): one dwordx4 per complex element
-__device__ __forceinline__ void st_sc1_b128(__amdgpu_buffer_rsrc_t r, int off, double2 v) {
-    v4u32 w;
-    w.x = __double2loint(v.x); w.y = __double2hiint(v.x); w.z = __double2loint(v.y); w.w = __double2hiint(v.y);
-    __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, 16);
-}
-__device__ __forceinline__ double2 ld_sc1_b128(__amdgpu_buffer_rsrc_t r, int off) {
-    const v4u32 w = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
-    return make_double2(__hiloint2double(w.y, w.x), __hiloint2double(w.w, w.z));
+// one granule: {tag, word} in ONE aligned 8-B sc1 store
+__device__ __forceinline__ void st_granule(unsigned long long* g, unsigned tag, unsigned word) {
+    __hip_atomic_store((gu64*)g, ((unsigned long long)tag << 32) | word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ double2 ld_sc1(const double2* p) {
@@ -74,7 +73,7 @@ struct SplitLayout {
     static constexpr int LDS = (LDS_STATE * 16 > SP_LDS_FORCE) ? LDS_STATE * 16 : SP_LDS_FORCE;
 };
 
-template <int N2, int CHI, bool B128>
+template <int N2, int CHI, bool GRAN>
 __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2* __restrict__ X,
                                                          unsigned* __restrict__ cnt, unsigned* __restrict__ err) {
     using L = SplitLayout<N2, CHI>;
@@ -85,6 +84,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
     // (output phase), PT partial sums — all indexed off smem so every access stays ds_*
     constexpr int OPO = 2 * E, RRO = OPO + N2 * N2, REDO = RRO + N2;
     __shared__ int s_abort;
+    if (threadIdx.x == 0) s_abort = 0;
 
     const int tid = threadIdx.x;
     const int tl = blockIdx.x / G, g = blockIdx.x - tl * G;
@@ -93,9 +93,12 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
     const long long wo = p.woff[t];
     const int sy = p.traj_sys[t];
     const int2 wn = fw_win(p, sy);  // pulse window: M, F, W outside it are the system's idle operators
-    double2* __restrict__ Xt = X + (size_t)t * 2 * E;
-    // descriptor over this trajectory's two exchange slots, from workgroup-uniform values only
-    const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(Xt, 0, 2 * E * 16, 0x00020000);
+    // exchange region of this trajectory: 2 slots x E elements x 4 granules x 8 B (GRAN) = 4 E double2; the
+    // counter form uses the first 2 E double2 of it
+    double2* __restrict__ Xt = X + (size_t)t * 4 * E;
+    unsigned long long* __restrict__ Gt = reinterpret_cast<unsigned long long*>(Xt);
+    // descriptor over this trajectory's granules, from workgroup-uniform values only (16-B sc1 loads of 2 granules)
+    const __amdgpu_buffer_rsrc_t rG = __builtin_amdgcn_make_buffer_rsrc(Xt, 0, 4 * E * 16, 0x00020000);
     unsigned* ct = cnt + (size_t)t * 32;  // one 128-B line per group counter
     const int n_end = we;
     constexpr int m2 = N2 * N2;
@@ -167,6 +170,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         for (int j = 0; j < KPER; ++j) sreg[j] = gld(S + (size_t)(kq * KPER + j) * CHI + dcol);
     };
     if (n_end > 0) fetch_slice(0);
+    int cur_slice = n_end > 0 ? p.sched[0] : -1;  // the slice index sreg holds
     bool pre = false;  // frow holds F(n)[g][tid] of the coming step
     for (int n = 0;; ++n) {
         // ---- trunk pre-pass: checkpoint of the state at the top of step n (M_b(n-1) still deferred), workgroup 0
@@ -216,68 +220,127 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         for (int j = 0; j < KPER; ++j) c_fma(acc, smem[rb + kq * KPER + j], sreg[j]);
         smem[REDO + tid] = acc;
         __syncthreads();
-        double2* Xn = Xt + (size_t)(n & 1) * E;
-        if (tid < CHI) {
-            double2 y = smem[REDO + tid];
+        if (GRAN) {
+            // thread q publishes word (q & 3) of element q >> 2 (every thread one granule when CHI = 64)
+            const unsigned ep = (unsigned)n + 1u;
+            for (int q = tid; q < 4 * CHI; q += SP_NT) {
+                const int el = q >> 2, wd = q & 3;
+                double2 y = smem[REDO + el];
 #pragma unroll
-            for (int q = 1; q < KG; ++q) y = c_add(y, smem[REDO + q * CHI + tid]);
-            if (B128) st_sc1_b128(rX, (int)(((size_t)(n & 1) * E + (size_t)g * CHI + tid) * 16), y);
-            else st_sc1(Xn + (size_t)g * CHI + tid, y);
+                for (int kg = 1; kg < KG; ++kg) y = c_add(y, smem[REDO + kg * CHI + el]);
+                const double v = (wd < 2) ? y.x : y.y;
+                const unsigned word = (wd & 1) ? (unsigned)__double2hiint(v) : (unsigned)__double2loint(v);
+                st_granule(Gt + ((size_t)(n & 1) * E + (size_t)g * CHI + el) * 4 + wd, ep, word);
+            }
+        } else {
+            double2* Xn = Xt + (size_t)(n & 1) * E;
+            if (tid < CHI) {
+                double2 y = smem[REDO + tid];
+#pragma unroll
+                for (int q = 1; q < KG; ++q) y = c_add(y, smem[REDO + q * CHI + tid]);
+                st_sc1(Xn + (size_t)g * CHI + tid, y);
+            }
+            // ---- arrive (every storing wave drained, then one lane); the wait for the group is below
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) __hip_atomic_fetch_add((gu32*)ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        // ---- arrive, prefetch the next step's slice row and fused operator, then wait for the group
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) __hip_atomic_fetch_add((gu32*)ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // ---- prefetch the next step's slice row (only when the schedule changes the slice: the repeated slice of
+        // ACE's _repeated / infinite PTs stays in registers) and fused operator row
         if (fz) output(n, fw_W(p, sy, wn, n, N2));  // off the group's critical path (workgroup 0 only)
-        if (n + 1 < n_end) fetch_slice(n + 1);
+        if (n + 1 < n_end) {
+            const int ns = p.sched[n + 1];
+            if (ns != cur_slice) { fetch_slice(n + 1); cur_slice = ns; }
+        }
         pre = p.fuse && n + 1 < n_end && !has_event(n + 1);
         if (pre && tid < N2) frow = gld(fw_F(p, sy, wn, n + 1, m2) + (size_t)g * N2 + tid);
-        if (tid < 64) {
-            const unsigned target = (unsigned)G * (unsigned)(n + 1);
+        if (GRAN) {
+            // ---- sweep: every element of the state, 2 x 16-B sc1 loads (2 granules each), re-read until its four
+            // tags are n + 1; each wave leaves when all its elements have arrived
+            constexpr int EPT = (E + SP_NT - 1) / SP_NT;
+            const unsigned ep = (unsigned)n + 1u;
+            unsigned pend = 0;
+#pragma unroll
+            for (int i = 0; i < EPT; ++i)
+                if (tid + SP_NT * i < E) pend |= 1u << i;
             unsigned spins = 0;
             bool ok = true;
-            while (__hip_atomic_load((gu32*)ct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            for (;;) {
+                // all of this pass's loads in flight before the first tag check
+                v4u32 ga[EPT], gb[EPT];
+#pragma unroll
+                for (int i = 0; i < EPT; ++i) {
+                    const int e = tid + SP_NT * i;
+                    const int off = (int)(((size_t)(n & 1) * E + (e < E ? e : 0)) * 32);
+                    if (pend & (1u << i)) {
+                        ga[i] = __builtin_amdgcn_raw_buffer_load_b128(rG, off, 0, 16);
+                        gb[i] = __builtin_amdgcn_raw_buffer_load_b128(rG, off + 16, 0, 16);
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < EPT; ++i) {
+                    if (!(pend & (1u << i))) continue;
+                    const v4u32 a = ga[i], b = gb[i];
+                    if (a.y == ep && a.w == ep && b.y == ep && b.w == ep) {
+                        smem[qo + tid + SP_NT * i] = make_double2(__hiloint2double((int)a.z, (int)a.x),
+                                                                  __hiloint2double((int)b.z, (int)b.x));
+                        pend &= ~(1u << i);
+                    }
+                }
+                if (__all(pend == 0)) break;
                 __builtin_amdgcn_s_sleep(1);
                 if (++spins > p.spin_limit) { ok = false; break; }
             }
-            if (tid == 0) {
-                s_abort = ok ? 0 : 1;
-                if (!ok) __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (!ok) {
+                s_abort = 1;
+                __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-        }
-        __syncthreads();
-        if (s_abort) return;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: payload loads are sc1
-        if (B128) {
-            for (int e = tid; e < E; e += SP_NT) smem[qo + e] = ld_sc1_b128(rX, (int)(((size_t)(n & 1) * E + e) * 16));
+            __syncthreads();
+            if (s_abort) return;
         } else {
+            if (tid < 64) {
+                const unsigned target = (unsigned)G * (unsigned)(n + 1);
+                unsigned spins = 0;
+                bool ok = true;
+                while (__hip_atomic_load((gu32*)ct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > p.spin_limit) { ok = false; break; }
+                }
+                if (tid == 0) {
+                    s_abort = ok ? 0 : 1;
+                    if (!ok) __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            __syncthreads();
+            if (s_abort) return;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: payload loads are sc1
+            const double2* Xn = Xt + (size_t)(n & 1) * E;
             for (int e = tid; e < E; e += SP_NT) smem[qo + e] = ld_sc1(Xn + e);
+            __syncthreads();
         }
-        __syncthreads();
     }
 }
 
-template <int N2, int CHI, bool B128>
-hipError_t launch_split_tb(int n_traj, const SweepParams& p, double2* X, unsigned* cnt, unsigned* err, hipStream_t s) {
+template <int N2, int CHI, bool GRAN>
+hipError_t launch_split_tg(int n_traj, const SweepParams& p, double2* X, unsigned* cnt, unsigned* err, hipStream_t s) {
     using L = SplitLayout<N2, CHI>;
     static_assert(L::LDS <= 160 * 1024, "LDS budget");
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)pt_split_kernel<N2, CHI, B128>,
+        hipError_t e = hipFuncSetAttribute((const void*)pt_split_kernel<N2, CHI, GRAN>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::LDS);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((pt_split_kernel<N2, CHI, B128>), dim3(n_traj * N2), dim3(SP_NT), L::LDS, s, p, X, cnt, err);
+    hipLaunchKernelGGL((pt_split_kernel<N2, CHI, GRAN>), dim3(n_traj * N2), dim3(SP_NT), L::LDS, s, p, X, cnt, err);
     return hipGetLastError();
 }
 
 template <int N2, int CHI>
 hipError_t launch_split_t(int n_traj, const SweepParams& p, double2* X, unsigned* cnt, unsigned* err, hipStream_t s) {
-    // p.split_b128 (PQD_SPLIT_B128=1 at plan creation): 16-B sc1 buffer accesses for the exchange (A/B switch;
-    // 0 = two 8-B atomics per element)
-    return p.split_b128 ? launch_split_tb<N2, CHI, true>(n_traj, p, X, cnt, err, s)
-                : launch_split_tb<N2, CHI, false>(n_traj, p, X, cnt, err, s);
+    // p.split_gran (PQD_SPLIT_GRAN, default 1): data-tagged granule exchange; 0 = the round-3 counter form
+    return p.split_gran ? launch_split_tg<N2, CHI, true>(n_traj, p, X, cnt, err, s)
+                        : launch_split_tg<N2, CHI, false>(n_traj, p, X, cnt, err, s);
 }
 
 template <int N2>
@@ -333,12 +396,17 @@ bool split_supported(int N2, int CHI, int n_traj, int n_cu) {
            (long long)n_traj * N2 <= n_cu;
 }
 
-// X: n_traj * 2 * N2 * CHI exchange buffer; cnt: n_traj * 32 counters and err, zeroed here before every launch.
+// X: n_traj * 4 * N2 * CHI double2 exchange buffer (granules, tags zeroed here); cnt: n_traj * 32 counters and err,
+// zeroed here before every launch.
 // chunk > 0: at most `chunk` trajectories per launch (each launch's groups co-resident), launched one after the other
 hipError_t launch_split(int N2, int CHI, int n_traj, const SweepParams& p, double2* X, unsigned* cnt,
                         unsigned* err, hipStream_t s, int chunk) {
     hipError_t e = hipMemsetAsync(cnt, 0, (size_t)n_traj * 32 * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
+    if (p.split_gran) {  // every granule tag 0: never a step's epoch (n + 1 >= 1)
+        e = hipMemsetAsync(X, 0, (size_t)n_traj * 4 * N2 * CHI * sizeof(double2), s);
+        if (e != hipSuccess) return e;
+    }
     e = hipMemsetAsync(err, 0, 4 * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
     if (chunk <= 0 || chunk > n_traj) chunk = n_traj;

@@ -80,11 +80,14 @@ def test_sweep_pt(N, chi):
 
 @pytest.mark.parametrize("N", [2, 3, 4, 5, 6])
 @pytest.mark.parametrize("chi", [16, 32, 64])
-@pytest.mark.parametrize("split", ["0", "2"])
+@pytest.mark.parametrize("split", ["0", "2", "2c"])
 def test_sweep_pt_split_groups(monkeypatch, N, chi, split):
     """small batches: each trajectory over N^2 workgroups gathering its state through global memory once per
-    step (pt_split.hip), forced (2) and off (0), with MTOs of every kind, ragged windows and several systems"""
-    monkeypatch.setenv("PQD_SPLIT", split)
+    step (pt_split.hip), forced (2: data-tagged granule exchange; 2c: the round-3 counter exchange) and off (0),
+    with MTOs of every kind (uneven work per group), ragged windows, several systems and a repeated slice (the
+    slice row kept in registers across steps)"""
+    monkeypatch.setenv("PQD_SPLIT", split[0])
+    monkeypatch.setenv("PQD_SPLIT_GRAN", "0" if split == "2c" else "1")
     systems = [H.random_system(N, n_steps=30, seed=40 + k)[0] for k in range(3)]
     grid = Grid(0.0, 0.1, 30)
     n_traj = max(1, min(7, 256 // (N * N)))
