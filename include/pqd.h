@@ -262,8 +262,9 @@ int pqd_tl_dynmap_pseudo(pqd_ctx* ctx, const pqd_c128* dm, int32_t n_maps, int32
 /* ---- PT generator factorizations (replaces the factorizations inside `ACE <generate.param>` with
  * `dont_propagate true` + `write_PT`, reference general_system.py:152-211; driven by pyaceqd_amd/ptgen_gpu.py,
  * whose host restatement is pyaceqd_amd/ptgen.py). Device pointers, column-major matrices (ld = rows), all work
- * enqueued on `stream` (a hipStream_t); both calls return after one device synchronisation (the rank / sweep
- * count decides what the caller does next).
+ * enqueued on `stream` (a hipStream_t). pqd_ptg_qr with pivot = 0 returns with its work still queued (its rank is
+ * min(m, n)); with pivot = 1, and pqd_ptg_jacobi, it synchronises with the stream (the rank / sweep count decides
+ * what the caller does next).
  *
  * pqd_ptg_qr: Householder QR of W (m x n, overwritten). pivot = 0: W = Q R with rank = min(m, n) (LAPACK zgeqrf
  * reflectors, R real diagonal). pivot = 1: column pivoting on the trailing column norms, stopping at the first step

@@ -73,6 +73,8 @@ __device__ __forceinline__ Refl make_refl(double2 alpha, double xn2) {
 struct QRArgs {
     double2* W;        // m x n column-major (ld = m), factorized in place: rows < k of a column hold R, column k's
                        //   rows > k keep x_k (v_k = (1; x_k * scale_k))
+    double2* X;        // the reflector columns: column k as it was when reflector k was made (rows < k: R, row k:
+                       //   alpha, rows > k: x_k). X == W for one-column steps; the two-column step keeps its own copy
     int m, n, kmax;    // kmax = min(m, n)
     int pivot;
     double tol2;       // pivot: stop when the largest trailing column norm^2 <= tol2
@@ -149,6 +151,8 @@ __global__ __launch_bounds__(256) void qr_step_kernel(QRArgs a, int k) {
         }
         if (a.pivot)
             for (int j = lane; j < a.n; j += 64) pout[j] = j < k ? pin[j] : phys(j);
+        if (a.X != a.W)
+            for (int i = lane; i < a.m; i += 64) a.X[(size_t)k * a.m + i] = x[i];
     }
     const int j = k + 1 + wave;
     if (j >= a.n) return;
@@ -180,6 +184,93 @@ __global__ __launch_bounds__(256) void qr_step_kernel(QRArgs a, int k) {
     }
 }
 
+// two reflectors per launch (plain QR only): every wave makes reflector k from column k, applies it to column k+1
+// on the fly and makes reflector k+1 from that (redundantly, no hand-off), then applies both to its own column in three
+// passes. Waves 0 and 1 store the two panel columns as the reflectors saw them into X (W's panel columns are read by
+// every wave of this launch, so they stay untouched). Half the launches of qr_step_kernel for the same arithmetic.
+__global__ __launch_bounds__(256) void qr_step2_kernel(QRArgs a, int k) {
+    const int lane = threadIdx.x & 63;
+    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int m = a.m;
+    const double2* c0 = a.W + (size_t)k * m;
+    const double2* c1 = a.W + (size_t)(k + 1) * m;
+    double xn0 = 0.0;
+    double2 w01 = c_zero();
+    for (int i = k + 1 + lane; i < m; i += 64) {
+        const double2 u = c0[i], v = c1[i];
+        xn0 += c_abs2(u);
+        w01.x += u.x * v.x + u.y * v.y;
+        w01.y += u.x * v.y - u.y * v.x;
+    }
+    xn0 = wsum(xn0);
+    w01 = wsum2(w01);
+    const Refl R0 = make_refl(c0[k], xn0);
+    // v0 = (1; c0 sc0): v0^H c1 = c1[k] + conj(sc0) sum conj(c0) c1
+    const double2 w0 = c_add(c1[k], c_cmul(R0.scale, w01));
+    const double2 ct01 = c_cmul(R0.tau, w0);
+    // c1' = c1 - ct01 v0 (rows >= k); reflector k+1 from rows >= k+1 of c1'
+    const double2 f01 = c_mul(ct01, R0.scale);  // c1'_i = c1_i - f01 c0_i for i > k
+    const double2 alpha1 = c_sub(c1[k + 1], c_mul(f01, c0[k + 1]));
+    double xn1 = 0.0;
+    for (int i = k + 2 + lane; i < m; i += 64) xn1 += c_abs2(c_sub(c1[i], c_mul(f01, c0[i])));
+    xn1 = wsum(xn1);
+    const Refl R1 = make_refl(alpha1, xn1);
+    if (wave == 0) {
+        if (lane == 0) {
+            a.tau[k] = R0.tau; a.scale[k] = R0.scale; a.beta[k] = R0.beta;
+            a.tau[k + 1] = R1.tau; a.scale[k + 1] = R1.scale; a.beta[k + 1] = R1.beta;
+        }
+        for (int i = lane; i < m; i += 64) a.X[(size_t)k * m + i] = c0[i];
+        return;
+    }
+    if (wave == 1) {
+        for (int i = lane; i < m; i += 64) {
+            double2 v = c1[i];
+            if (i == k) v = c_sub(v, ct01);
+            else if (i > k) v = c_sub(v, c_mul(f01, c0[i]));
+            a.X[(size_t)(k + 1) * m + i] = v;
+        }
+        return;
+    }
+    const int j = k + wave;  // waves 2.. -> columns k+2..
+    if (j >= a.n) return;
+    double2* col = a.W + (size_t)j * m;
+    // pass A: w = v0^H c_j
+    double2 sA = c_zero();
+    for (int i = k + 1 + lane; i < m; i += 64) {
+        const double2 u = c0[i], v = col[i];
+        sA.x += u.x * v.x + u.y * v.y;
+        sA.y += u.x * v.y - u.y * v.x;
+    }
+    sA = wsum2(sA);
+    const double2 ck = col[k], ck1 = col[k + 1];
+    const double2 ctA = c_cmul(R0.tau, c_add(ck, c_cmul(R0.scale, sA)));
+    const double2 fA = c_mul(ctA, R0.scale);  // (H_k^H c_j)_i = c_i - fA c0_i for i > k
+    // pass B: w = v1^H (H_k^H c_j), v1 = (1 at k+1; (c1_i - f01 c0_i) sc1 for i > k+1)
+    double2 sB = c_zero();
+    for (int i = k + 2 + lane; i < m; i += 64) {
+        const double2 u0 = c0[i];
+        const double2 v1 = c_sub(c1[i], c_mul(f01, u0));
+        const double2 y = c_sub(col[i], c_mul(fA, u0));
+        sB.x += v1.x * y.x + v1.y * y.y;
+        sB.y += v1.x * y.y - v1.y * y.x;
+    }
+    sB = wsum2(sB);
+    const double2 yk1 = c_sub(ck1, c_mul(fA, c0[k + 1]));
+    const double2 ctB = c_cmul(R1.tau, c_add(yk1, c_cmul(R1.scale, sB)));
+    const double2 fB = c_mul(ctB, R1.scale);
+    // pass C: c_j <- H_{k+1}^H H_k^H c_j
+    for (int i = k + 2 + lane; i < m; i += 64) {
+        const double2 u0 = c0[i];
+        const double2 v1 = c_sub(c1[i], c_mul(f01, u0));
+        col[i] = c_sub(c_sub(col[i], c_mul(fA, u0)), c_mul(fB, v1));
+    }
+    if (lane == 0) {
+        col[k] = c_sub(ck, ctA);
+        col[k + 1] = c_sub(yk1, ctB);
+    }
+}
+
 // R (rank x n, column-major, ld = rank) in pivoted column order; perm_out = the final permutation
 __global__ void qr_extract_r_kernel(QRArgs a, int rank, double2* R, int* perm_out) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -189,7 +280,8 @@ __global__ void qr_extract_r_kernel(QRArgs a, int rank, double2* R, int* perm_ou
     const int j = idx / rank, i = idx - j * rank;
     const int c = a.pivot ? pf[j] : j;
     double2 v;
-    if (i < j) v = a.W[(size_t)c * a.m + i];
+    // reflector columns (j < rank) as their reflector saw them (X); columns past the rank only in W
+    if (i < j) v = (j < rank ? a.X : a.W)[(size_t)c * a.m + i];
     else if (i == j) v = make_double2(a.beta[i], 0.0);
     else v = c_zero();
     R[(size_t)j * rank + i] = v;
@@ -213,7 +305,7 @@ __global__ __launch_bounds__(256) void qf_apply_kernel(QRArgs a, int rank, const
     double2* col = Q + (size_t)j * a.m;
     for (int i = min(j, i1 - 1); i >= i0; --i) {
         const int pc = a.pivot ? perm_final[i] : i;
-        const double2* x = a.W + (size_t)pc * a.m;
+        const double2* x = a.X + (size_t)pc * a.m;
         const double2 sc = a.scale[i], tau = a.tau[i];
         const double2 ci0 = col[i];
         double2 s = c_zero();
@@ -370,9 +462,24 @@ struct JacArgs {
     double2* V;   // n x n, accumulated
     int n, nn;    // nn = n rounded up to even (index n is a dummy player)
     double tol;
-    double zero2; // a column with |x|^2 < zero2 is numerically zero: its pairs are never rotated
+    const double* zero2; // device word: a column with |x|^2 < *zero2 is numerically zero, never rotated
     int* count;   // rotations in this sweep
 };
+
+// *zero2 = zero_tol^2 ||X||_F^2 (one workgroup; rotations leave ||X||_F unchanged)
+__global__ __launch_bounds__(1024) void jac_zero2_kernel(const double2* X, int n, double zt2, double* zero2) {
+    __shared__ double part[16];
+    double s = 0.0;
+    for (size_t i = threadIdx.x; i < (size_t)n * n; i += 1024) s += c_abs2(X[i]);
+    s = wsum(s);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < 16; ++w) t += part[w];
+        *zero2 = zt2 * t;
+    }
+}
 
 __device__ __forceinline__ void jac_pair(int t, int i, int nn, int& p, int& q) {
     auto L = [&](int s) { return s == 0 ? 0 : ((s - 1 + t) % (nn - 1)) + 1; };
@@ -434,19 +541,20 @@ __global__ __launch_bounds__(256) void jac_round_kernel(JacArgs a, int t) {
     jac_pair(t, i, a.nn, p, q);
     if (q >= a.n) return;
     const bool rot = jac_rotate(a.X + (size_t)p * a.n, a.X + (size_t)q * a.n, a.V + (size_t)p * a.n,
-                                a.V + (size_t)q * a.n, a.n, a.n, a.tol, a.zero2, lane);
+                                a.V + (size_t)q * a.n, a.n, a.n, a.tol, *a.zero2, lane);
     if (rot && lane == 0) atomicAdd(a.count, 1);
 }
 
 // single workgroup: X and V in LDS (2 n^2 <= QS_MAX), all sweeps in one launch
 __global__ __launch_bounds__(QS_THREADS) void jac_small_kernel(double2* Xg, double2* Vg, int n, double tol,
-                                                              double zero2, int max_sweeps, int* sweeps_out) {
+                                                              const double* zero2p, int max_sweeps, int* sweeps_out) {
     extern __shared__ double2 sm[];
     double2* X = sm;
     double2* V = sm + n * n;
     __shared__ int s_cnt;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = QS_THREADS / 64;
     const int nn = n + (n & 1);
+    const double zero2 = *zero2p;
     for (int idx = tid; idx < n * n; idx += QS_THREADS) {
         X[idx] = Xg[idx];
         const int j = idx / n, i = idx - j * n;
@@ -563,10 +671,14 @@ extern "C" int pqd_ptg_qr(void* stream, pqd_c128* Wp, int32_t m, int32_t n, int3
     const int kmax = std::min(m, n);
     const double tol2 = pivot ? tol * tol : -1.0;
     void* base = nullptr;
+    // two reflectors per launch for plain QRs on the multi-workgroup path (PQD_PTG_PAIR=0: one per launch)
+    const char* ep = getenv("PQD_PTG_PAIR");
+    const bool small = small_ok() && (size_t)m * n <= (size_t)QS_MAX && n <= 256;
+    const bool pairs = !pivot && !small && kmax >= 2 && !(ep && atoi(ep) == 0);
     const size_t b_tau = al(kmax * sizeof(double2)), b_beta = al(kmax * sizeof(double)),
                  b_perm = al(2 * (size_t)n * sizeof(int)), b_norm = al(2 * (size_t)n * sizeof(double)),
-                 b_ctrl = al(64 * sizeof(int));
-    PCHK(scratch(2 * b_tau + b_beta + b_perm + b_norm + b_ctrl, &base));
+                 b_ctrl = al(64 * sizeof(int)), b_x = pairs ? al((size_t)m * kmax * sizeof(double2)) : 0;
+    PCHK(scratch(2 * b_tau + b_beta + b_perm + b_norm + b_ctrl + b_x, &base));
     char* c = static_cast<char*>(base);
     QRArgs a;
     a.W = W; a.m = m; a.n = n; a.kmax = kmax; a.pivot = pivot ? 1 : 0; a.tol2 = tol2;
@@ -575,13 +687,18 @@ extern "C" int pqd_ptg_qr(void* stream, pqd_c128* Wp, int32_t m, int32_t n, int3
     a.beta = reinterpret_cast<double*>(c); c += b_beta;
     a.perm = reinterpret_cast<int*>(c); c += b_perm;
     a.norms = reinterpret_cast<double*>(c); c += b_norm;
-    a.ctrl = reinterpret_cast<int*>(c);
+    a.ctrl = reinterpret_cast<int*>(c); c += b_ctrl;
+    a.X = pairs ? reinterpret_cast<double2*>(c) : W;
     int* d_rank = a.ctrl + 8;
-    if (small_ok() && (size_t)m * n <= (size_t)QS_MAX && n <= 256) {
+    if (small) {
         PCHK(small_attrs());
         hipLaunchKernelGGL(qr_small_kernel, dim3(1), dim3(QS_THREADS), (size_t)m * n * sizeof(double2), s, W, m, n,
                            a.pivot, tol2, Q, R, perm_out, d_rank);
         PCHK(hipGetLastError());
+        if (!pivot) {  // the rank of a plain QR is min(m, n): no host round trip, the caller's work stays queued
+            *rank_out = kmax;
+            return PQD_OK;
+        }
         int rank = 0;
         PCHK(hipMemcpyAsync(&rank, d_rank, sizeof(int), hipMemcpyDeviceToHost, s));
         PCHK(hipStreamSynchronize(s));
@@ -590,14 +707,23 @@ extern "C" int pqd_ptg_qr(void* stream, pqd_c128* Wp, int32_t m, int32_t n, int3
     }
     const int wpb = 4;
     hipLaunchKernelGGL(qr_init_kernel, dim3((n + wpb - 1) / wpb), dim3(64 * wpb), 0, s, a);
-    for (int k = 0; k < kmax; ++k) {
-        const int nw = std::max(1, n - k - 1);
-        hipLaunchKernelGGL(qr_step_kernel, dim3((nw + wpb - 1) / wpb), dim3(64 * wpb), 0, s, a, k);
+    for (int k = 0; k < kmax;) {
+        if (pairs && k + 1 < kmax) {
+            const int nw = 2 + std::max(0, n - k - 2);
+            hipLaunchKernelGGL(qr_step2_kernel, dim3((nw + wpb - 1) / wpb), dim3(64 * wpb), 0, s, a, k);
+            k += 2;
+        } else {
+            const int nw = std::max(1, n - k - 1);
+            hipLaunchKernelGGL(qr_step_kernel, dim3((nw + wpb - 1) / wpb), dim3(64 * wpb), 0, s, a, k);
+            k += 1;
+        }
     }
     PCHK(hipGetLastError());
-    int rank = 0;
-    PCHK(hipMemcpyAsync(&rank, a.ctrl, sizeof(int), hipMemcpyDeviceToHost, s));
-    PCHK(hipStreamSynchronize(s));
+    int rank = kmax;
+    if (pivot) {  // the stopping step decides the rank: one host round trip
+        PCHK(hipMemcpyAsync(&rank, a.ctrl, sizeof(int), hipMemcpyDeviceToHost, s));
+        PCHK(hipStreamSynchronize(s));
+    }
     const int tot = std::max(rank * n, n);
     hipLaunchKernelGGL(qr_extract_r_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, a, rank, R, perm_out);
     if (rank > 0) {
@@ -626,16 +752,10 @@ extern "C" int pqd_ptg_jacobi(void* stream, pqd_c128* Xp, int32_t n, pqd_c128* V
     void* base = nullptr;
     PCHK(scratch(al(64 * sizeof(int)), &base));
     int* cnt = static_cast<int*>(base);
+    double* zero2 = reinterpret_cast<double*>(cnt + 8);
     int sweeps = 0;
     // zero threshold relative to the Frobenius norm (rotation-invariant): |x_j| < zero_tol * ||X||_F
-    double fro2 = 0.0;
-    {
-        std::vector<double2> h((size_t)n * n);
-        PCHK(hipMemcpyAsync(h.data(), X, h.size() * sizeof(double2), hipMemcpyDeviceToHost, s));
-        PCHK(hipStreamSynchronize(s));
-        for (const double2& v : h) fro2 += v.x * v.x + v.y * v.y;
-    }
-    const double zero2 = zero_tol * zero_tol * fro2;
+    hipLaunchKernelGGL(jac_zero2_kernel, dim3(1), dim3(1024), 0, s, X, n, zero_tol * zero_tol, zero2);
     if (small_ok() && 2 * (size_t)n * n <= (size_t)QS_MAX) {
         PCHK(small_attrs());
         hipLaunchKernelGGL(jac_small_kernel, dim3(1), dim3(QS_THREADS), 2 * (size_t)n * n * sizeof(double2), s, X, V,
