@@ -19,13 +19,17 @@ Contractions, stacking and reshapes are torch operations on the device (rocBLAS 
 The public entry points mirror ptgen's: GaussianPTBuilderGPU (step / closure / stationary_slice),
 build_gaussian_pt_gpu, qd_phonon_pt_gpu. They return the same ProcessTensor (host numpy arrays)."""
 import ctypes as C
-import math
+import os
 
 import numpy as np
 
 from . import _lib
 from . import ptgen
 from .engine import ProcessTensor
+
+
+_DEBUG = bool(int(os.environ.get("PQD_PTG_DEBUG", "0") or 0))
+_STATS = []  # (kind, sizes...) per factorization when PQD_PTG_DEBUG=1 (scripts/bench_ptgen.py --stats)
 
 
 def _torch():
@@ -55,6 +59,8 @@ def qr_cols(Wc, pivot=False, tol=0.0):
                                      float(tol), C.c_void_p(Q.data_ptr()), C.c_void_p(R.data_ptr()),
                                      C.c_void_p(perm.data_ptr()), C.byref(rank)))
     k = rank.value
+    if _DEBUG:
+        _STATS.append(("qrcp" if pivot else "qr", m, n, k))
     return Q[: k * m].view(k, m), R[: k * n].view(n, k), perm.long(), k
 
 
@@ -79,6 +85,8 @@ def jacobi_cols(Xc, tol=None, max_sweeps=60, zero_tol=1e-16):
                                          C.byref(sw)))
     if sw.value >= max_sweeps:
         raise _lib.PQDError(f"pqd_ptg_jacobi: no convergence in {max_sweeps} sweeps (n = {n})")
+    if _DEBUG:
+        _STATS.append(("jacobi", n, sw.value))
     return X, V, sig
 
 

@@ -27,7 +27,10 @@ def main():
     ap.add_argument("--steps", type=int, default=0, help="stop after N steps (0: the whole PT, 2K + stationary)")
     ap.add_argument("--host", action="store_true", help="also time the host generator")
     ap.add_argument("--tail", default="qrcp")
+    ap.add_argument("--stats", action="store_true", help="factorization shapes / Jacobi sweeps of the last step")
     a = ap.parse_args()
+    if a.stats:
+        os.environ["PQD_PTG_DEBUG"] = "1"
     import numpy as np
     from pyaceqd_amd import ptgen, ptgen_gpu
     for name in a.case.split(","):
@@ -48,6 +51,8 @@ def main():
             t0 = time.perf_counter()
             tl = t0
             for n in range(n_tot):
+                if a.stats and side == "gpu":
+                    ptgen_gpu._STATS.clear()
                 b.step()
                 if n % 20 == 0 or n == n_tot - 1:
                     sync()
@@ -56,6 +61,15 @@ def main():
                     print(f"{name} {side} step {n + 1}/{2 * K} {t - t0:8.2f} s (last block {t - tl:6.2f} s) "
                           f"bond {b.r} tail max {max(tails or [1])}", flush=True)
                     tl = t
+            if a.stats and side == "gpu":
+                import collections
+                st = ptgen_gpu._STATS
+                cnt = collections.Counter(x[0] for x in st)
+                big = sorted((x for x in st if x[0] != "jacobi"), key=lambda x: -x[1] * x[2])[:12]
+                print(f"STATS last step: {dict(cnt)}; jacobi (n, sweeps): {[x[1:] for x in st if x[0] == 'jacobi']}; "
+                      f"largest QRs (m, n, rank): {[x[1:] for x in big]}; "
+                      f"column steps: {sum(min(x[1], x[2]) if x[0] == 'qr' else x[3] for x in st if x[0] != 'jacobi')}",
+                      flush=True)
             if n_tot == 2 * K:
                 b.stationary_slice()
             sync()
