@@ -268,8 +268,14 @@ int pqd_tl_dynmap_pseudo(pqd_ctx* ctx, const pqd_c128* dm, int32_t n_maps, int32
  *
  * pqd_ptg_qr: Householder QR of W (m x n, overwritten). pivot = 0: W = Q R with rank = min(m, n) (LAPACK zgeqrf
  * reflectors, R real diagonal). pivot = 1: column pivoting on the trailing column norms, stopping at the first step
- * whose largest trailing column norm is <= tol (a rank-revealing truncation): W P ~= Q R. Outputs: Q (m x rank),
- * R (rank x n, columns in pivoted order), perm (n: column j of W P is column perm[j] of W), *rank (host). */
+ * whose largest trailing column norm is <= tol (a rank-revealing truncation): W P ~= Q R; tol < 0 means |tol| times
+ * the largest column norm of W (found on the device: no host pass over W). Outputs: Q (m x rank),
+ * R (rank x n, columns in pivoted order), perm (n: column j of W P is column perm[j] of W), *rank (host).
+ * Kernel choice (environment, read per call; every combination is parity-tested): PQD_PTG_SMALL=0 (no
+ * single-workgroup LDS kernel), PQD_PTG_WG=0 (per-wave column steps instead of workgroup-per-column steps with the
+ * columns in registers), PQD_PTG_PAIR=0 (one reflector per launch), PQD_PTG_BLOCKED=1 (plain QRs factorized in
+ * panels of 32 columns with a compact-WY trailing update), PQD_PTG_QFB=0 (Q by the per-wave reflector kernel
+ * instead of blocks of 32 reflectors). */
 int pqd_ptg_qr(void* stream, pqd_c128* W, int32_t m, int32_t n, int32_t pivot, double tol, pqd_c128* Q,
                pqd_c128* R, int32_t* perm, int32_t* rank);
 /* pqd_ptg_jacobi: one-sided Jacobi SVD of a square n x n X (overwritten): X V = U diag(sigma), columns rotated

@@ -49,7 +49,9 @@ def qr_cols(Wc, pivot=False, tol=0.0):
     rank). pivot: column pivoting with a stop at trailing column norm <= tol (absolute)."""
     torch = _torch()
     n, m = Wc.shape
-    W = Wc.resolve_conj().resolve_neg().contiguous().clone()
+    W = Wc.resolve_conj().resolve_neg().contiguous()  # a conj view / strided view is materialised here ...
+    if W.data_ptr() == Wc.data_ptr():
+        W = W.clone()                                 # ... else copy: W is overwritten
     kmax = min(m, n)
     Q = torch.empty(kmax * m, dtype=torch.complex128, device=W.device)
     R = torch.empty(max(kmax, 1) * n, dtype=torch.complex128, device=W.device)
@@ -61,7 +63,7 @@ def qr_cols(Wc, pivot=False, tol=0.0):
     k = rank.value
     if _DEBUG:
         _STATS.append(("qrcp" if pivot else "qr", m, n, k))
-    return Q[: k * m].view(k, m), R[: k * n].view(n, k), perm.long(), k
+    return Q[: k * m].view(k, m), R[: k * n].view(n, k), (perm.long() if pivot else perm), k
 
 
 def jacobi_cols(Xc, tol=None, max_sweeps=60, zero_tol=1e-16):
@@ -76,7 +78,9 @@ def jacobi_cols(Xc, tol=None, max_sweeps=60, zero_tol=1e-16):
     n = Xc.shape[0]
     if tol is None:
         tol = max(16, n) * 2.220446049250313e-16
-    X = Xc.resolve_conj().resolve_neg().contiguous().clone()
+    X = Xc.resolve_conj().resolve_neg().contiguous()
+    if X.data_ptr() == Xc.data_ptr():
+        X = X.clone()
     V = torch.empty((n, n), dtype=torch.complex128, device=X.device)
     sig = torch.empty(n, dtype=torch.float64, device=X.device)
     sw = C.c_int32(0)
@@ -103,13 +107,12 @@ def svd(A, rank_tol=1e-14):
     r, c = A.shape
     Wc = A.conj() if r <= c else A.T             # rows of Wc = columns of W (tall: m = max(r, c), n = min(r, c))
     n, m = Wc.shape
-    cmax = float(torch.sqrt(torch.max(torch.sum(Wc.real ** 2 + Wc.imag ** 2, dim=1))))
-    if cmax == 0.0:                                # a zero block: one zero singular value
+    Q1c, R1c, perm, k1 = qr_cols(Wc, pivot=True, tol=-rank_tol)   # rank_tol x the largest column norm
+    if k1 == 0:                                    # a zero block: one zero singular value
         U = torch.zeros((r, 1), dtype=A.dtype, device=A.device)
         Vh = torch.zeros((1, c), dtype=A.dtype, device=A.device)
         U[0, 0] = Vh[0, 0] = 1.0
         return U, torch.zeros(1, dtype=torch.float64, device=A.device), Vh
-    Q1c, R1c, perm, k1 = qr_cols(Wc, pivot=True, tol=rank_tol * cmax)
     B = torch.zeros((k1, n), dtype=A.dtype, device=A.device)
     B[:, perm] = R1c.T
     Q2c, R2c, _, k2 = qr_cols(B.conj())          # B^H = Q2 R2 (n x k1, k1 x k1)
@@ -167,12 +170,12 @@ def _compress(mps, threshold, max_bond, tail_threshold=None, tail_max_bond=None,
             mps[j] = u[:, :kk].reshape(cl, P, kk)
             carry = s[:kk, None].to(vh.dtype) * vh[:kk]
         else:
-            cmax = float(torch.sqrt(torch.max(torch.sum(M.real ** 2 + M.imag ** 2, dim=0))))
-            Qc, Rc, perm, kk = qr_cols(M.T.contiguous(), pivot=True, tol=tthr * cmax)
-            if kk == 0:
+            Qc, Rc, perm, kk = qr_cols(M.T, pivot=True, tol=-tthr)  # tthr x the largest column norm
+            if kk == 0:                            # M == 0: keep one (zero-weight) bond direction
                 kk = 1
-                Qc, Rc, perm, _ = qr_cols(M.T.contiguous(), pivot=True, tol=0.0)
-                Qc, Rc = Qc[:1], Rc[:, :1]
+                Qc = torch.zeros((1, M.shape[0]), dtype=M.dtype, device=M.device)
+                Qc[0, 0] = 1.0
+                Rc = torch.zeros((M.shape[1], 1), dtype=M.dtype, device=M.device)
             if tail_max_bond and kk > tail_max_bond:
                 kk = tail_max_bond
                 Qc, Rc = Qc[:kk], Rc[:, :kk]

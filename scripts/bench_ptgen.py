@@ -70,6 +70,11 @@ def main():
                       f"largest QRs (m, n, rank): {[x[1:] for x in big]}; "
                       f"column steps: {sum(min(x[1], x[2]) if x[0] == 'qr' else x[3] for x in st if x[0] != 'jacobi')}",
                       flush=True)
+                small = [x for x in st if x[0] != "jacobi" and x[1] * x[2] <= 8192 and x[2] <= 256]
+                hist = collections.Counter((x[0], "wide" if x[1] < x[2] else "tall", min(x[1], 256) // 32 * 32,
+                                            min(x[2], 256) // 32 * 32) for x in small)
+                print(f"SMALL (single-workgroup) calls: {len(small)}; by (kind, shape, m//32*32, n//32*32): "
+                      f"{sorted(hist.items(), key=lambda t: -t[1])[:24]}", flush=True)
             if n_tot == 2 * K:
                 b.stationary_slice()
             sync()

@@ -44,7 +44,8 @@ def _rand(rng, m, n, rank=None, scale=None):
 
 
 @pytest.mark.parametrize("small", ["1", "0"])
-@pytest.mark.parametrize("m,n", [(7, 5), (5, 7), (195, 39), (40, 30), (300, 120), (930, 369)])
+@pytest.mark.parametrize("m,n", [(7, 5), (5, 7), (195, 39), (40, 30), (300, 120), (930, 369), (600, 13), (100, 80),
+                                 (64, 128)])
 def test_ptg_qr_matches_lapack(monkeypatch, small, m, n):
     from pyaceqd_amd import ptgen_gpu
     monkeypatch.setenv("PQD_PTG_SMALL", small)
@@ -60,8 +61,63 @@ def test_ptg_qr_matches_lapack(monkeypatch, small, m, n):
     assert np.max(np.abs(R - Rn)) < 1e-12 * np.max(np.abs(Rn))
 
 
+@pytest.mark.parametrize("mode", ["wg", "wg_blocked", "wave", "wave_qf"])
+@pytest.mark.parametrize("m,n,kind", [(300, 120, "rand"), (930, 369, "rand"), (2955, 636, "graded"), (640, 273, "rand"),
+                                      (500, 97, "lowrank"), (200, 200, "graded"), (129, 65, "rand"), (5000, 70, "rand")])
+def test_ptg_qr_paths_match_lapack(monkeypatch, mode, m, n, kind):
+    """plain QR on the multi-workgroup path, every kernel combination: workgroup-per-column step kernels (columns in
+    registers; m > 4096 falls back to the per-wave kernels), the blocked factorization (panels of 32, trailing update
+    V T^H V^H A), the per-wave kernels, and Q from blocks of 32 reflectors (default) or the per-wave Q kernel. Q
+    orthonormal, W = Q R, R equal to LAPACK's (same reflectors), on random, graded (1 .. 1e-13) and numerically
+    low-rank blocks"""
+    from pyaceqd_amd import ptgen_gpu
+    monkeypatch.setenv("PQD_PTG_SMALL", "0")
+    monkeypatch.setenv("PQD_PTG_WG", "0" if mode.startswith("wave") else "1")
+    monkeypatch.setenv("PQD_PTG_BLOCKED", "1" if mode == "wg_blocked" else "0" if mode == "wg" else "-1")
+    monkeypatch.setenv("PQD_PTG_QFB", "0" if mode == "wave_qf" else "1")
+    rng = np.random.default_rng(m * 3 + n)
+    if kind == "lowrank":
+        W = _rand(rng, m, n, rank=n // 4)
+    elif kind == "graded":
+        W = _rand(rng, m, n, scale=np.logspace(0, -13, n))
+    else:
+        W = _rand(rng, m, n)
+    Qc, Rc, perm, k = ptgen_gpu.qr_cols(_dev(W.T))
+    Q, R = Qc.T.cpu().numpy(), Rc.T.cpu().numpy()
+    assert k == n and np.array_equal(perm.cpu().numpy(), np.arange(n))
+    assert np.max(np.abs(Q.conj().T @ Q - np.eye(k))) < 1e-13
+    assert np.max(np.abs(Q @ R - W)) < 1e-13 * np.max(np.abs(W)) * np.sqrt(m)
+    assert np.max(np.abs(np.tril(R, -1))) == 0.0
+    Rn = np.linalg.qr(W, mode="r")
+    assert np.max(np.abs(R - Rn)) < 1e-12 * np.max(np.abs(Rn))
+
+
+@pytest.mark.parametrize("wg", ["1", "0"])
+@pytest.mark.parametrize("m,n,rank", [(1205, 300, 120), (400, 250, None), (5000, 90, 40)])
+def test_ptg_qrcp_step_kernels(monkeypatch, wg, m, n, rank):
+    """the rank-revealing pivoted QR on the workgroup-per-column and the per-wave step kernels: the same pivots
+    and rank, Q orthonormal, W P = Q R + E within the tolerance"""
+    from pyaceqd_amd import ptgen_gpu
+    monkeypatch.setenv("PQD_PTG_SMALL", "0")
+    monkeypatch.setenv("PQD_PTG_WG", wg)
+    rng = np.random.default_rng(m + 7 * n)
+    W = _rand(rng, m, n, rank=rank, scale=None if rank else np.logspace(0, -14, n))
+    tol = 1e-10 * np.max(np.linalg.norm(W, axis=0))
+    Qc, Rc, perm, k = ptgen_gpu.qr_cols(_dev(W.T), pivot=True, tol=tol)
+    Q, R, p = Qc.T.cpu().numpy(), Rc.T.cpu().numpy(), perm.cpu().numpy()
+    assert sorted(p) == list(range(n))
+    assert np.max(np.abs(Q.conj().T @ Q - np.eye(k))) < 1e-12
+    assert np.linalg.norm(W[:, p] - Q @ R) <= np.sqrt(n - k + 1) * tol * 1.01 + 1e-13 * np.linalg.norm(W)
+    if rank is not None:
+        assert k == rank
+    monkeypatch.setenv("PQD_PTG_WG", "0" if wg == "1" else "1")
+    _, _, perm2, k2 = ptgen_gpu.qr_cols(_dev(W.T), pivot=True, tol=tol)
+    assert k2 == k and np.array_equal(perm2.cpu().numpy()[:k], p[:k])
+
+
 @pytest.mark.parametrize("small", ["1", "0"])
-@pytest.mark.parametrize("m,n,rank", [(80, 39, 13), (60, 40, None), (1205, 300, 120), (400, 250, None)])
+@pytest.mark.parametrize("m,n,rank", [(80, 39, 13), (60, 40, None), (1205, 300, 120), (400, 250, None), (700, 11, 5),
+                                      (150, 50, None)])
 def test_ptg_qrcp_rank_revealing(monkeypatch, small, m, n, rank):
     """column-pivoted QR stopping at a norm tolerance: Q orthonormal, pivots non-increasing, W P = Q R + E with
     ||E||_F <= sqrt(n - k) tol, and for a numerically rank-r matrix the rank found is r"""
@@ -82,15 +138,18 @@ def test_ptg_qrcp_rank_revealing(monkeypatch, small, m, n, rank):
         assert k == rank
 
 
-@pytest.mark.parametrize("small", ["1", "0"])
+@pytest.mark.parametrize("small", ["1", "0", "0-rounds"])
 @pytest.mark.parametrize("r,c,graded", [(6, 9, False), (40, 200, True), (384, 1350, False), (300, 90, True),
-                                         (120, 120, True), (45, 101, "lowrank"), (201, 700, "lowrank")])
+                                         (120, 120, True), (45, 101, "lowrank"), (201, 700, "lowrank"),
+                                         (1100, 700, True)])
 def test_ptg_svd_matches_lapack(monkeypatch, small, r, c, graded):
     """thin SVD vs LAPACK on random, graded (1 .. 1e-13) and numerically low-rank blocks (odd sizes: the Jacobi
     tournament's dummy player; rank 1/4: three quarters of the columns at the rounding floor, as the stacked
-    generator blocks are)"""
+    generator blocks are). Jacobi on the single-workgroup kernel, the persistent grid kernel (n <= 1024, default)
+    and one launch per round ("0-rounds", also what n > 1024 uses)"""
     from pyaceqd_amd import ptgen_gpu
-    monkeypatch.setenv("PQD_PTG_SMALL", small)
+    monkeypatch.setenv("PQD_PTG_SMALL", small[0])
+    monkeypatch.setenv("PQD_PTG_JPERSIST", "0" if small == "0-rounds" else "1")
     rng = np.random.default_rng(r * 7 + c)
     k = min(r, c)
     if graded == "lowrank":
