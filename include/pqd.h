@@ -269,7 +269,8 @@ int pqd_tl_dynmap_pseudo(pqd_ctx* ctx, const pqd_c128* dm, int32_t n_maps, int32
  * pqd_ptg_qr: Householder QR of W (m x n, overwritten). pivot = 0: W = Q R with rank = min(m, n) (LAPACK zgeqrf
  * reflectors, R real diagonal). pivot = 1: column pivoting on the trailing column norms, stopping at the first step
  * whose largest trailing column norm is <= tol (a rank-revealing truncation): W P ~= Q R; tol < 0 means |tol| times
- * the largest column norm of W (found on the device: no host pass over W). Outputs: Q (m x rank),
+ * the largest column norm of W (found on the device: no host pass over W). pivot = 2: the same, with R returned in
+ * W's own column order (R P^T: column perm[j] of the output is column j of R), so that W ~= Q R directly. Outputs: Q (m x rank),
  * R (rank x n, columns in pivoted order), perm (n: column j of W P is column perm[j] of W), *rank (host).
  * Kernel choice (environment, read per call; every combination is parity-tested): PQD_PTG_SMALL=0 (no
  * single-workgroup LDS kernel), PQD_PTG_WG=0 (per-wave column steps instead of workgroup-per-column steps with the

@@ -100,10 +100,12 @@ struct SweepParams {
     int umax;                //   a unit with slice < 0 ends a wave's list; NULL: rows a = wave + k BT
     int trpre;               // 1: traces one lane per (trajectory, output, row), W rows fetched a step ahead
     int ablate;              // diagnostics only (PQD_ABLATE): 1 skip PT, 2 skip column phases, 4 skip outputs
-    int split_gran;          // split groups: data-tagged granule exchange (default 1; PQD_SPLIT_GRAN=0: counter form)
+    int split_gran;          // split groups: data-tagged granule exchange (PQD_SPLIT_GRAN=1; default 0: counter form)
     unsigned* flags;         // bit 0: a non-finite output value (set by launch_check_finite at synchronize)
     unsigned spin_limit;     // split groups: polls before a wait for the peers times out (PQD_SPLIT_SPIN, tests)
     int traj_base;           // split groups: trajectory of group 0 (a batch run as several co-resident launches)
+    int split_xcd;           // split groups, set per launch: > 0 = trajectories in this launch, each group's workgroups
+                             //   dealt onto one XCD (blocks b with equal b % 8; speed only, PQD_SPLIT_XCD=0 off)
     int n_steps;             // grid steps (operand prefetch bound)
     int n_blk;               // blocks of the launch (quad kernel: quads; tail workgroups check it)
     int qprio;               // quad kernel wave priorities (PQD_QPRIO, A/B): bit 0 first half of the grid above the

@@ -1025,7 +1025,10 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     sp.blk_act = P->blk_act.p; sp.blk_src = P->blk_src.p;
     sp.traj_sys = P->traj_sys.p; sp.m_stride = (long long)2 * ns * m2; sp.wbeg = P->wbeg.p; sp.wend = P->wend.p;
     { const char* ab = getenv("PQD_ABLATE"); sp.ablate = ab ? atoi(ab) : 0; }
-    { const char* b1 = getenv("PQD_SPLIT_GRAN"); sp.split_gran = (b1 && atoi(b1) == 0) ? 0 : 1; }
+    // exchange form: counter (default; with the XCD-grouped grid C3 runs 5.02 us per step against 5.33 for the granules,
+    // profiles/r04/split/xcd/) or data-tagged granules (PQD_SPLIT_GRAN=1)
+    { const char* b1 = getenv("PQD_SPLIT_GRAN"); sp.split_gran = (b1 && atoi(b1) == 1) ? 1 : 0; }
+    { const char* b2 = getenv("PQD_SPLIT_XCD"); sp.split_xcd = (b2 && atoi(b2) == 0) ? 0 : 1; }
     // polls of a split group's counter before the wait counts as a timeout (~0.1 s); PQD_SPLIT_SPIN overrides
     // it (tests provoke the batched fallback with 0)
     { const char* sl = getenv("PQD_SPLIT_SPIN"); sp.spin_limit = sl ? (unsigned)strtoul(sl, nullptr, 10) : (1u << 22); }

@@ -87,7 +87,16 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
     if (threadIdx.x == 0) s_abort = 0;
 
     const int tid = threadIdx.x;
-    const int tl = blockIdx.x / G, g = blockIdx.x - tl * G;
+    int tl = blockIdx.x / G, g = blockIdx.x - tl * G;
+    if (p.split_xcd > 0) {
+        // XCD-grouped grid (launch_split_tg): block b sits in XCD slot b % 8 under the observed round-robin dealing;
+        // group tl = slot + 8 (b / 8 / G) keeps all G workgroups of a group in one slot, so the group's hand-offs
+        // stay in one L2 when the dealing holds. Placement is speed only: the exchange is the same at any placement.
+        const int xs = blockIdx.x & 7, loc = blockIdx.x >> 3;
+        tl = xs + 8 * (loc / G);
+        g = loc - (loc / G) * G;
+        if (tl >= p.split_xcd) return;  // an unused block (before any shared state is touched)
+    }
     const int t = p.traj_base + tl;
     const int wb = p.wbeg[t], we = p.wend[t];
     const long long wo = p.woff[t];
@@ -332,13 +341,23 @@ hipError_t launch_split_tg(int n_traj, const SweepParams& p, double2* X, unsigne
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((pt_split_kernel<N2, CHI, GRAN>), dim3(n_traj * N2), dim3(SP_NT), L::LDS, s, p, X, cnt, err);
+    // XCD-grouped grid when every XCD slot can hold its groups at one workgroup per CU (32 CUs per XCD on MI355X):
+    // 8 slots x ceil(n_traj / 8) groups x G blocks, the blocks of missing groups return at once
+    const int per_slot = (n_traj + 7) / 8;
+    SweepParams q = p;
+    unsigned nb = (unsigned)(n_traj * N2);
+    q.split_xcd = 0;
+    if (p.split_xcd && per_slot * N2 <= 32) {
+        q.split_xcd = n_traj;
+        nb = 8u * (unsigned)(per_slot * N2);
+    }
+    hipLaunchKernelGGL((pt_split_kernel<N2, CHI, GRAN>), dim3(nb), dim3(SP_NT), L::LDS, s, q, X, cnt, err);
     return hipGetLastError();
 }
 
 template <int N2, int CHI>
 hipError_t launch_split_t(int n_traj, const SweepParams& p, double2* X, unsigned* cnt, unsigned* err, hipStream_t s) {
-    // p.split_gran (PQD_SPLIT_GRAN, default 1): data-tagged granule exchange; 0 = the round-3 counter form
+    // p.split_gran (PQD_SPLIT_GRAN=1): data-tagged granule exchange; default 0 = the counter form
     return p.split_gran ? launch_split_tg<N2, CHI, true>(n_traj, p, X, cnt, err, s)
                         : launch_split_tg<N2, CHI, false>(n_traj, p, X, cnt, err, s);
 }

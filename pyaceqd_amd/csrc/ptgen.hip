@@ -303,7 +303,8 @@ __global__ __launch_bounds__(256) void qr_step2_kernel(QRArgs a, int k) {
 }
 
 // R (rank x n, column-major, ld = rank) in pivoted column order; perm_out = the final permutation
-__global__ void qr_extract_r_kernel(QRArgs a, int rank, double2* R, int* perm_out) {
+// unperm: column j of R (pivoted order) is written as column perm[j] (R P^T, the original column order)
+__global__ void qr_extract_r_kernel(QRArgs a, int rank, double2* R, int* perm_out, int unperm) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     const int* pf = a.perm + (size_t)(rank & 1) * a.n;
     if (idx < a.n) perm_out[idx] = a.pivot ? pf[idx] : idx;
@@ -315,7 +316,7 @@ __global__ void qr_extract_r_kernel(QRArgs a, int rank, double2* R, int* perm_ou
     if (i < j) v = (j < rank ? a.X : a.W)[(size_t)c * a.m + i];
     else if (i == j) v = make_double2(a.beta[i], 0.0);
     else v = c_zero();
-    R[(size_t)j * rank + i] = v;
+    R[(size_t)(unperm ? c : j) * rank + i] = v;
 }
 
 // Q = H_0 ... H_{rank-1} [I; 0]  (m x rank): init, then blocks of QF_RB reflectors applied in descending order
@@ -751,7 +752,7 @@ constexpr int QS_THREADS = 1024;
 template <int QE>
 __global__ __launch_bounds__(QS_THREADS) void qr_small_kernel(const double2* Win, int m, int n, int pivot, double tol2,
                                                              double rel2, double2* Q, double2* R, int* perm_out,
-                                                             int* rank_out) {
+                                                             int* rank_out, int unperm, int diag) {
     // one barrier per column step: every wave finds the pivot and builds the reflector itself (redundantly, from
     // LDS), then updates its trailing columns; the permutation is double-buffered by step parity (wave 0 writes the
     // next one), so no wave waits for a serial pivot / reflector phase
@@ -776,7 +777,7 @@ __global__ __launch_bounds__(QS_THREADS) void qr_small_kernel(const double2* Win
         }
     __syncthreads();
     int k = 0;
-    for (; k < kmax; ++k) {
+    for (; k < ((diag & 2) ? 0 : kmax); ++k) {  // diag (PQD_PTG_DIAG, timing only): 2 = no column steps
         const int* pin = s_perm[k & 1];
         int* pout = s_perm[(k + 1) & 1];
         const double* nin = s_norm[k & 1];
@@ -801,39 +802,96 @@ __global__ __launch_bounds__(QS_THREADS) void qr_small_kernel(const double2* Win
         }
         auto phys = [&](int j) { return j == k ? pin[p] : (j == p ? pin[k] : pin[j]); };
         const double2* x = A + phys(k) * m;
-        double xn = 0.0;
-        for (int i = k + 1 + lane; i < m; i += 64) xn += c_abs2(x[i]);
-        xn = wsum(xn);
-        const Refl Rf = make_refl(x[k], xn);
-        if (wave == 0) {
-            if (lane == 0) { s_tau[k] = Rf.tau; s_scale[k] = Rf.scale; s_beta[k] = Rf.beta; }
-            for (int j = lane; j < n; j += 64) pout[j] = j < k ? pin[j] : phys(j);
-        }
-        const double2 sc = Rf.scale, tau = Rf.tau;
-        for (int j = k + 1 + wave; j < n; j += nw) {
-            const int cidx = phys(j);
-            double2* col = A + cidx * m;
-            const double2 ck = col[k];
-            double2 sacc = c_zero();
-            for (int i = k + 1 + lane; i < m; i += 64) {
-                const double2 v = c_mul(x[i], sc);
-                const double2 ci = col[i];
-                sacc.x += v.x * ci.x + v.y * ci.y;
-                sacc.y += v.x * ci.y - v.y * ci.x;
+        if constexpr (QE > 0) {
+            // the pivot column in registers for the whole step; each trailing column: one round of LDS loads
+            double2 xr[QE];
+            double xn = 0.0;
+#pragma unroll
+            for (int e = 0; e < QE; ++e) {
+                const int r = lane + 64 * e;
+                xr[e] = r < m ? x[r] : c_zero();
+                if (r > k && r < m) xn += c_abs2(xr[e]);
             }
-            sacc = wsum2(sacc);
-            sacc = c_add(sacc, ck);
-            const double2 ct = c_cmul(tau, sacc);
-            double nn = 0.0;
-            for (int i = k + 1 + lane; i < m; i += 64) {
-                const double2 ci = c_sub(col[i], c_mul(ct, c_mul(x[i], sc)));
-                col[i] = ci;
-                nn += c_abs2(ci);
+            xn = wsum(xn);
+            const Refl Rf = make_refl(x[k], xn);
+            if (wave == 0) {
+                if (lane == 0) { s_tau[k] = Rf.tau; s_scale[k] = Rf.scale; s_beta[k] = Rf.beta; }
+                for (int j = lane; j < n; j += 64) pout[j] = j < k ? pin[j] : phys(j);
             }
-            if (pivot) nn = wsum(nn);  // trailing norms only steer the pivot search
-            if (lane == 0) {
-                col[k] = c_sub(ck, ct);
-                nout[cidx] = nn;
+#pragma unroll
+            for (int e = 0; e < QE; ++e) {
+                const int r = lane + 64 * e;
+                xr[e] = r > k && r < m ? c_mul(xr[e], Rf.scale) : c_zero();  // v below the diagonal
+            }
+            for (int j = k + 1 + wave; j < n; j += nw) {
+                const int cidx = phys(j);
+                double2* col = A + cidx * m;
+                double2 cv[QE];
+#pragma unroll
+                for (int e = 0; e < QE; ++e) {
+                    const int r = lane + 64 * e;
+                    cv[e] = r < m ? col[r] : c_zero();
+                }
+                const double2 ck = col[k];
+                double2 sacc = c_zero();
+#pragma unroll
+                for (int e = 0; e < QE; ++e) {
+                    sacc.x += xr[e].x * cv[e].x + xr[e].y * cv[e].y;
+                    sacc.y += xr[e].x * cv[e].y - xr[e].y * cv[e].x;
+                }
+                sacc = c_add(wsum2(sacc), ck);
+                const double2 ct = c_cmul(Rf.tau, sacc);
+                double nn = 0.0;
+#pragma unroll
+                for (int e = 0; e < QE; ++e) {
+                    const int r = lane + 64 * e;
+                    if (r > k && r < m) {
+                        const double2 ci = c_sub(cv[e], c_mul(ct, xr[e]));
+                        col[r] = ci;
+                        nn += c_abs2(ci);
+                    }
+                }
+                if (pivot) nn = wsum(nn);  // trailing norms only steer the pivot search
+                if (lane == 0) {
+                    col[k] = c_sub(ck, ct);
+                    nout[cidx] = nn;
+                }
+            }
+        } else {
+            double xn = 0.0;
+            for (int i = k + 1 + lane; i < m; i += 64) xn += c_abs2(x[i]);
+            xn = wsum(xn);
+            const Refl Rf = make_refl(x[k], xn);
+            if (wave == 0) {
+                if (lane == 0) { s_tau[k] = Rf.tau; s_scale[k] = Rf.scale; s_beta[k] = Rf.beta; }
+                for (int j = lane; j < n; j += 64) pout[j] = j < k ? pin[j] : phys(j);
+            }
+            const double2 sc = Rf.scale, tau = Rf.tau;
+            for (int j = k + 1 + wave; j < n; j += nw) {
+                const int cidx = phys(j);
+                double2* col = A + cidx * m;
+                const double2 ck = col[k];
+                double2 sacc = c_zero();
+                for (int i = k + 1 + lane; i < m; i += 64) {
+                    const double2 v = c_mul(x[i], sc);
+                    const double2 ci = col[i];
+                    sacc.x += v.x * ci.x + v.y * ci.y;
+                    sacc.y += v.x * ci.y - v.y * ci.x;
+                }
+                sacc = wsum2(sacc);
+                sacc = c_add(sacc, ck);
+                const double2 ct = c_cmul(tau, sacc);
+                double nn = 0.0;
+                for (int i = k + 1 + lane; i < m; i += 64) {
+                    const double2 ci = c_sub(col[i], c_mul(ct, c_mul(x[i], sc)));
+                    col[i] = ci;
+                    nn += c_abs2(ci);
+                }
+                if (pivot) nn = wsum(nn);  // trailing norms only steer the pivot search
+                if (lane == 0) {
+                    col[k] = c_sub(ck, ct);
+                    nout[cidx] = nn;
+                }
             }
         }
         __syncthreads();
@@ -846,10 +904,11 @@ __global__ __launch_bounds__(QS_THREADS) void qr_small_kernel(const double2* Win
     for (int idx = tid; idx < rank * n; idx += QS_THREADS) {
         const int j = idx / rank, i = idx - j * rank;
         const int c = s_pf[j];
-        R[idx] = i < j ? A[c * m + i] : (i == j ? make_double2(s_beta[i], 0.0) : c_zero());
+        R[unperm ? c * rank + i : idx] = i < j ? A[c * m + i] : (i == j ? make_double2(s_beta[i], 0.0) : c_zero());
     }
     for (int j = tid; j < n; j += QS_THREADS) perm_out[j] = s_pf[j];
     if (tid == 0) *rank_out = rank;
+    if (diag & 1) return;  // timing only: no Q
     // Q (m x rank), one wave per column, reflectors descending. QE > 0: the column lives in registers (QE rows per
     // lane, m <= 64 QE) and goes to global memory once; QE == 0: in global memory (a round trip per reflector)
     for (int j = wave; j < rank; j += nw) {
@@ -1356,6 +1415,7 @@ extern "C" int pqd_ptg_qr(void* stream, pqd_c128* Wp, int32_t m, int32_t n, int3
     const int kmax = std::min(m, n);
     // tol >= 0: absolute; tol < 0: relative to the largest column norm of W (found on the device, no host pass)
     const double tol2 = pivot && tol >= 0.0 ? tol * tol : -1.0;
+    const bool unperm = pivot == 2;  // R returned in the original column order (R P^T)
     const double rel2 = pivot && tol < 0.0 ? tol * tol : 0.0;
     void* base = nullptr;
     const bool small = small_ok() && (size_t)m * n <= (size_t)QS_MAX && n <= 256;
@@ -1391,9 +1451,10 @@ extern "C" int pqd_ptg_qr(void* stream, pqd_c128* Wp, int32_t m, int32_t n, int3
     if (small) {
         PCHK(small_attrs());
         const size_t lds = (size_t)m * n * sizeof(double2);
+        const int diag = env_int("PQD_PTG_DIAG", 0);
         const int qe = m <= 64 ? 1 : m <= 128 ? 2 : m <= 256 ? 4 : m <= 512 ? 8 : 0;
 #define PQD_QS(QEV) hipLaunchKernelGGL(qr_small_kernel<QEV>, dim3(1), dim3(QS_THREADS), lds, s, W, m, n, a.pivot, \
-                                       tol2, rel2, Q, R, perm_out, d_rank)
+                                       tol2, rel2, Q, R, perm_out, d_rank, unperm ? 1 : 0, diag)
         switch (qe) {
             case 1: PQD_QS(1); break;
             case 2: PQD_QS(2); break;
@@ -1436,7 +1497,8 @@ extern "C" int pqd_ptg_qr(void* stream, pqd_c128* Wp, int32_t m, int32_t n, int3
         PCHK(hipStreamSynchronize(s));
     }
     const int tot = std::max(rank * n, n);
-    hipLaunchKernelGGL(qr_extract_r_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, a, rank, R, perm_out);
+    hipLaunchKernelGGL(qr_extract_r_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, a, rank, R, perm_out,
+                       unperm ? 1 : 0);
     if (rank > 0) {
         const size_t mq = (size_t)m * rank;
         hipLaunchKernelGGL(qf_init_kernel, dim3((unsigned)((mq + 255) / 256)), dim3(256), 0, s, Q, m, rank);

@@ -43,7 +43,7 @@ def _stream(torch):
     return C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
-def qr_cols(Wc, pivot=False, tol=0.0):
+def qr_cols(Wc, pivot=False, tol=0.0, unperm=False):
     """Householder QR of W (m x n) given as Wc (n, m): row j of Wc is column j of W (a column-major buffer).
     Returns (Qc (rank, m): row i = column i of Q, Rc (n, rank): row j = column j of R (pivoted order), perm (n,),
     rank). pivot: column pivoting with a stop at trailing column norm <= tol (absolute)."""
@@ -57,7 +57,8 @@ def qr_cols(Wc, pivot=False, tol=0.0):
     R = torch.empty(max(kmax, 1) * n, dtype=torch.complex128, device=W.device)
     perm = torch.empty(n, dtype=torch.int32, device=W.device)
     rank = C.c_int32(0)
-    _lib.check(_lib.lib().pqd_ptg_qr(_stream(torch), C.c_void_p(W.data_ptr()), int(m), int(n), 1 if pivot else 0,
+    _lib.check(_lib.lib().pqd_ptg_qr(_stream(torch), C.c_void_p(W.data_ptr()), int(m), int(n),
+                                     (2 if unperm else 1) if pivot else 0,
                                      float(tol), C.c_void_p(Q.data_ptr()), C.c_void_p(R.data_ptr()),
                                      C.c_void_p(perm.data_ptr()), C.byref(rank)))
     k = rank.value
@@ -94,6 +95,10 @@ def jacobi_cols(Xc, tol=None, max_sweeps=60, zero_tol=1e-16):
     return X, V, sig
 
 
+_JZERO = float(os.environ.get("PQD_PTG_JZERO", "1e-16") or 1e-16)  # Jacobi zero-column threshold (A/B runs)
+_JT = os.environ.get("PQD_PTG_JT", "1") == "1"                     # Jacobi on R2^H (DV), 0: on R2 (A/B runs)
+
+
 def svd(A, rank_tol=1e-14):
     """Thin SVD of A (r x c, device complex128): (U (r, k), S (k,), Vh (k, c)), S descending, k = the numerical
     rank at rank_tol (directions below rank_tol x the largest column norm are dropped: far below any truncation
@@ -107,19 +112,24 @@ def svd(A, rank_tol=1e-14):
     r, c = A.shape
     Wc = A.conj() if r <= c else A.T             # rows of Wc = columns of W (tall: m = max(r, c), n = min(r, c))
     n, m = Wc.shape
-    Q1c, R1c, perm, k1 = qr_cols(Wc, pivot=True, tol=-rank_tol)   # rank_tol x the largest column norm
+    Q1c, R1c, perm, k1 = qr_cols(Wc, pivot=True, tol=-rank_tol, unperm=True)  # rank_tol x the largest column norm
     if k1 == 0:                                    # a zero block: one zero singular value
         U = torch.zeros((r, 1), dtype=A.dtype, device=A.device)
         Vh = torch.zeros((1, c), dtype=A.dtype, device=A.device)
         U[0, 0] = Vh[0, 0] = 1.0
         return U, torch.zeros(1, dtype=torch.float64, device=A.device), Vh
-    B = torch.zeros((k1, n), dtype=A.dtype, device=A.device)
-    B[:, perm] = R1c.T
+    B = R1c.T                                      # R1 P^T (k1 x n)
     Q2c, R2c, _, k2 = qr_cols(B.conj())          # B^H = Q2 R2 (n x k1, k1 x k1)
-    Xc, Vc, sig = jacobi_cols(R2c)
-    o = torch.argsort(sig, descending=True, stable=True)
-    UW = (Vc[o] @ Q1c).T                           # (m, k1): columns Q1 v_o
-    VhW = (Xc[o] @ Q2c).conj()                     # (k1, n): rows (Q2 uhat_o)^H
+    if _JT:                                        # Jacobi on X = R2^H: X V = Uhat S, W = (Q1 Uhat) S (Q2 V)^H
+        Xc, Vc, sig = jacobi_cols(R2c.conj().T, zero_tol=_JZERO)
+        o = torch.argsort(sig, descending=True, stable=True)
+        UW = (Xc[o] @ Q1c).T
+        VhW = (Vc[o] @ Q2c).conj()
+    else:
+        Xc, Vc, sig = jacobi_cols(R2c, zero_tol=_JZERO)
+        o = torch.argsort(sig, descending=True, stable=True)
+        UW = (Vc[o] @ Q1c).T                       # (m, k1): columns Q1 v_o
+        VhW = (Xc[o] @ Q2c).conj()                 # (k1, n): rows (Q2 uhat_o)^H
     if r <= c:                                     # W = A^H
         return VhW.conj().T, sig[o], UW.conj().T
     return UW, sig[o], VhW
@@ -144,9 +154,11 @@ def _rcanon(mps):
     for j in range(len(mps) - 1, 0, -1):
         T = mps[j]
         cl, P, cr = T.shape
-        Qc, Rc, _, k = qr_cols(T.reshape(cl, P * cr).conj())
-        mps[j] = Qc.conj().reshape(k, P, cr)
-        mps[j - 1] = torch.tensordot(mps[j - 1], Rc.conj(), dims=([2], [0]))
+        # T = R^H Q^H from the QR of T^H; Householder QR commutes with conjugation (zlarfg: beta real, tau and v
+        # conjugate), so the QR of T^T = conj(T^H) hands over conj(Q), conj(R) without materialising T^H
+        Qc, Rc, _, k = qr_cols(T.reshape(cl, P * cr))
+        mps[j] = Qc.reshape(k, P, cr)
+        mps[j - 1] = torch.tensordot(mps[j - 1], Rc, dims=([2], [0]))
 
 
 def _compress(mps, threshold, max_bond, tail_threshold=None, tail_max_bond=None, tail="qrcp"):
@@ -170,7 +182,7 @@ def _compress(mps, threshold, max_bond, tail_threshold=None, tail_max_bond=None,
             mps[j] = u[:, :kk].reshape(cl, P, kk)
             carry = s[:kk, None].to(vh.dtype) * vh[:kk]
         else:
-            Qc, Rc, perm, kk = qr_cols(M.T, pivot=True, tol=-tthr)  # tthr x the largest column norm
+            Qc, Rc, perm, kk = qr_cols(M.T, pivot=True, tol=-tthr, unperm=True)  # tthr x the largest column norm
             if kk == 0:                            # M == 0: keep one (zero-weight) bond direction
                 kk = 1
                 Qc = torch.zeros((1, M.shape[0]), dtype=M.dtype, device=M.device)
@@ -180,8 +192,7 @@ def _compress(mps, threshold, max_bond, tail_threshold=None, tail_max_bond=None,
                 kk = tail_max_bond
                 Qc, Rc = Qc[:kk], Rc[:, :kk]
             mps[j] = Qc.T.reshape(cl, P, kk)
-            carry = torch.zeros((kk, cr), dtype=M.dtype, device=M.device)
-            carry[:, perm] = Rc.T
+            carry = Rc.T                           # R P^T
         cur = torch.tensordot(carry, mps[j + 1], dims=([1], [0]))
     mps[-1] = cur
     return U, mps

@@ -80,14 +80,16 @@ def test_sweep_pt(N, chi):
 
 @pytest.mark.parametrize("N", [2, 3, 4, 5, 6])
 @pytest.mark.parametrize("chi", [16, 32, 64])
-@pytest.mark.parametrize("split", ["0", "2", "2c"])
+@pytest.mark.parametrize("split", ["0", "2g", "2c", "2c-noxcd"])
 def test_sweep_pt_split_groups(monkeypatch, N, chi, split):
     """small batches: each trajectory over N^2 workgroups gathering its state through global memory once per
-    step (pt_split.hip), forced (2: data-tagged granule exchange; 2c: the round-3 counter exchange) and off (0),
-    with MTOs of every kind (uneven work per group), ragged windows, several systems and a repeated slice (the
-    slice row kept in registers across steps)"""
+    step (pt_split.hip), forced (2g: data-tagged granule exchange; 2c: the counter exchange, the default; both
+    with each group's workgroups dealt onto one XCD; 2c-noxcd: the plain grid) and off (0), with MTOs of every
+    kind (uneven work per group), ragged windows, several systems and a repeated slice (the slice row kept in
+    registers across steps)"""
     monkeypatch.setenv("PQD_SPLIT", split[0])
-    monkeypatch.setenv("PQD_SPLIT_GRAN", "0" if split == "2c" else "1")
+    monkeypatch.setenv("PQD_SPLIT_GRAN", "1" if split == "2g" else "0")
+    monkeypatch.setenv("PQD_SPLIT_XCD", "0" if split.endswith("noxcd") else "1")
     systems = [H.random_system(N, n_steps=30, seed=40 + k)[0] for k in range(3)]
     grid = Grid(0.0, 0.1, 30)
     n_traj = max(1, min(7, 256 // (N * N)))

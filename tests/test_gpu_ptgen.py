@@ -136,6 +136,12 @@ def test_ptg_qrcp_rank_revealing(monkeypatch, small, m, n, rank):
     assert np.all(d[1:] <= d[:-1] * (1 + 1e-12))
     if rank is not None:
         assert k == rank
+    # pivot = 2 (unperm): R in W's own column order, relative tolerance found on the device
+    Qc2, Rc2, perm2, k2 = ptgen_gpu.qr_cols(_dev(W.T), pivot=True, tol=-1e-10, unperm=True)
+    Q2, R2 = Qc2.T.cpu().numpy(), Rc2.T.cpu().numpy()
+    assert k2 == k and np.array_equal(perm2.cpu().numpy(), p)
+    assert np.max(np.abs(R2[:, p] - R)) == 0.0 and np.max(np.abs(Q2 - Q)) == 0.0
+    assert np.linalg.norm(W - Q2 @ R2) <= np.sqrt(n - k + 1) * tol * 1.01 + 1e-13 * np.linalg.norm(W)
 
 
 @pytest.mark.parametrize("small", ["1", "0", "0-rounds"])
