@@ -30,6 +30,7 @@ from .engine import ProcessTensor
 
 _DEBUG = bool(int(os.environ.get("PQD_PTG_DEBUG", "0") or 0))
 _STATS = []  # (kind, sizes...) per factorization when PQD_PTG_DEBUG=1 (scripts/bench_ptgen.py --stats)
+RETRIES = []  # (n, attempt) of every boundary SVD whose Jacobi needed another attempt (svd below)
 
 
 def _torch():
@@ -110,6 +111,12 @@ def svd(A, rank_tol=1e-14):
     R2 V = Uhat S."""
     torch = _torch()
     r, c = A.shape
+    # scale to max |a_ij| = 1 (on the device, no host pass): the generator's boundary blocks reach 1e81 and more (the
+    # future-influence MPS norm grows like sqrt(P)^K), where the Jacobi test |x_p^H x_q| > tol sqrt(|x_p|^2 |x_q|^2)
+    # overflows; LAPACK scales the same way
+    amax = torch.amax(A.abs())
+    sc = torch.where(amax > 0, amax, torch.ones_like(amax))
+    A = A / sc
     Wc = A.conj() if r <= c else A.T             # rows of Wc = columns of W (tall: m = max(r, c), n = min(r, c))
     n, m = Wc.shape
     Q1c, R1c, perm, k1 = qr_cols(Wc, pivot=True, tol=-rank_tol, unperm=True)  # rank_tol x the largest column norm
@@ -120,19 +127,33 @@ def svd(A, rank_tol=1e-14):
         return U, torch.zeros(1, dtype=torch.float64, device=A.device), Vh
     B = R1c.T                                      # R1 P^T (k1 x n)
     Q2c, R2c, _, k2 = qr_cols(B.conj())          # B^H = Q2 R2 (n x k1, k1 x k1)
-    if _JT:                                        # Jacobi on X = R2^H: X V = Uhat S, W = (Q1 Uhat) S (Q2 V)^H
-        Xc, Vc, sig = jacobi_cols(R2c.conj().T, zero_tol=_JZERO)
-        o = torch.argsort(sig, descending=True, stable=True)
-        UW = (Xc[o] @ Q1c).T
-        VhW = (Vc[o] @ Q2c).conj()
-    else:
-        Xc, Vc, sig = jacobi_cols(R2c, zero_tol=_JZERO)
-        o = torch.argsort(sig, descending=True, stable=True)
-        UW = (Vc[o] @ Q1c).T                       # (m, k1): columns Q1 v_o
-        VhW = (Xc[o] @ Q2c).conj()                 # (k1, n): rows (Q2 uhat_o)^H
+    attempts = [(_JT, _JZERO), (not _JT, _JZERO), (_JT, max(_JZERO, 1e-13))]
+    for ia, (jt, zt) in enumerate(attempts):
+        # the two orientations give the same SVD; R2^H (Drmac-Veselic) usually needs fewer sweeps (8 against 10 on
+        # the biexciton boundary blocks). A block on which one does not converge is tried on the other, then with
+        # columns below 1e-13 ||X||_F left unrotated (far below any truncation threshold the generator uses)
+        try:
+            if jt:                                 # Jacobi on X = R2^H: X V = Uhat S, W = (Q1 Uhat) S (Q2 V)^H
+                Xc, Vc, sig = jacobi_cols(R2c.conj().T, zero_tol=zt)
+                o = torch.argsort(sig, descending=True, stable=True)
+                UW = (Xc[o] @ Q1c).T
+                VhW = (Vc[o] @ Q2c).conj()
+            else:                                  # Jacobi on R2: R2 V = Uhat S, W = (Q1 V) S (Q2 Uhat)^H
+                Xc, Vc, sig = jacobi_cols(R2c, zero_tol=zt)
+                o = torch.argsort(sig, descending=True, stable=True)
+                UW = (Vc[o] @ Q1c).T               # (m, k1): columns Q1 v_o
+                VhW = (Xc[o] @ Q2c).conj()         # (k1, n): rows (Q2 uhat_o)^H
+            break
+        except _lib.PQDError as e:
+            if "no convergence" not in str(e) or ia == len(attempts) - 1:
+                if os.environ.get("PQD_PTG_DUMP"):     # the block, for offline analysis
+                    np.save(os.environ["PQD_PTG_DUMP"], R2c.cpu().numpy())
+                raise
+            RETRIES.append((int(R2c.shape[0]), ia))
+    S = sig[o] * sc
     if r <= c:                                     # W = A^H
-        return VhW.conj().T, sig[o], UW.conj().T
-    return UW, sig[o], VhW
+        return VhW.conj().T, S, UW.conj().T
+    return UW, S, VhW
 
 
 def _keep(S_host, threshold, max_k):

@@ -180,6 +180,20 @@ def test_ptg_svd_matches_lapack(monkeypatch, small, r, c, graded):
     assert np.max(np.abs((U * S[None, :]) @ Vh - A)) < 1e-13 * Sn[0] * np.sqrt(max(r, c))
 
 
+@pytest.mark.parametrize("scale", [1e-150, 1e81, 1e150])
+def test_ptg_svd_extreme_scale(scale):
+    """the generator's boundary blocks reach 1e81 and beyond (the future-influence MPS norm grows like sqrt(P)^K):
+    the device SVD scales internally, so squared column norms and the Jacobi test never overflow (found on the
+    K = 205 biexciton PT, where the unscaled Jacobi did not converge)"""
+    from pyaceqd_amd import ptgen_gpu
+    rng = np.random.default_rng(5)
+    A0 = _rand(rng, 384, 700, scale=np.logspace(0, -11, 700))
+    U, S, Vh = (x.cpu().numpy() for x in ptgen_gpu.svd(_dev(A0 * scale)))
+    Sn = np.linalg.svd(A0, compute_uv=False)
+    assert np.max(np.abs(S / scale - Sn[:len(S)])) < 1e-13 * Sn[0]
+    assert np.max(np.abs((U * (S / scale)[None, :]) @ Vh - A0)) < 1e-13 * Sn[0] * np.sqrt(700)
+
+
 # ---------------------------------------------------------------------------------------------------- the PT
 def influence(pt, paths):
     """bond0 Q_s(1)[g(a_1)] ... Q_s(n)[g(a_n)] c_s(n) for each path of Liouville indices (the slice schedule of
