@@ -239,7 +239,9 @@ __global__ __launch_bounds__(64) void mc_tau_pipe_kernel(MapChainParams p) {
 // results agree to rounding (the Fortran goldens and the pipelined kernel, PQD_MC_BLOCKED=0).
 // ---------------------------------------------------------------------------------------------
 // the map at position q of the shared sequence: mode 0 dm_tl(:, :, q + 1); mode 1 (calc_onetime_parallel_block) the
-// periodic sequence jj = q mod n_tb + 1 -> dm_block(:, :, jj) for jj <= n_map, else dm_s (propagate_tau.f90:270-287)
+// periodic sequence jj = q mod n_tb + 1 -> dm_block(:, :, jj) for jj <= n_map, else dm_s (propagate_tau.f90:270-287).
+// The blocked mode-1 path treats every position past q_s as dm_s: that holds only for n_map <= n_tb, and the host
+// (pqd_host.cpp, blocked-kernel choice) runs the map-by-map kernels when n_map > n_tb.
 __device__ __forceinline__ const double2* map_at(const MapChainParams& p, int q, int M2) {
     if (p.mode == 0) return p.dmA + (size_t)q * M2;
     if (q >= p.q_s) return p.dm_s;
