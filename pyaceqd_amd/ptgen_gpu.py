@@ -20,6 +20,7 @@ The public entry points mirror ptgen's: GaussianPTBuilderGPU (step / closure / s
 build_gaussian_pt_gpu, qd_phonon_pt_gpu. They return the same ProcessTensor (host numpy arrays)."""
 import ctypes as C
 import os
+import time
 
 import numpy as np
 
@@ -29,6 +30,8 @@ from .engine import ProcessTensor
 
 
 _DEBUG = bool(int(os.environ.get("PQD_PTG_DEBUG", "0") or 0))
+# PQD_PTG_PHASES=1: wall time per compression phase (synchronising: diagnostics only, scripts/bench_ptgen.py)
+_PHASES = {"rcanon": 0.0, "svd": 0.0, "lr": 0.0} if os.environ.get("PQD_PTG_PHASES") == "1" else None
 _STATS = []  # (kind, sizes...) per factorization when PQD_PTG_DEBUG=1 (scripts/bench_ptgen.py --stats)
 RETRIES = []  # (n, attempt) of every boundary SVD whose Jacobi needed another attempt (svd below)
 
@@ -186,10 +189,20 @@ def _compress(mps, threshold, max_bond, tail_threshold=None, tail_max_bond=None,
     """ptgen._compress on the device. Returns (U, mps') with U the phase-fixed isometry of the boundary SVD."""
     torch = _torch()
     tthr = threshold if tail_threshold is None else tail_threshold
+    tm = _PHASES is not None
+    if tm:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
     _rcanon(mps)
+    if tm:
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
     T = mps[0]
     L, P, cr = T.shape
     U, S, Vh = svd(T.reshape(L, P * cr))
+    if tm:
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
     Sh = S.cpu().numpy()
     k = _keep(Sh, threshold, max_bond)
     U, Vh = _fix_phase(U[:, :k], Vh[:k])
@@ -216,6 +229,12 @@ def _compress(mps, threshold, max_bond, tail_threshold=None, tail_max_bond=None,
             carry = Rc.T                           # R P^T
         cur = torch.tensordot(carry, mps[j + 1], dims=([1], [0]))
     mps[-1] = cur
+    if tm:
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        _PHASES["rcanon"] += t1 - t0
+        _PHASES["svd"] += t2 - t1
+        _PHASES["lr"] += t3 - t2
     return U, mps
 
 

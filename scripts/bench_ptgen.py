@@ -82,6 +82,8 @@ def main():
             full = el if n_tot == 2 * K else el * (2 * K + 1) / n_tot
             if side == "gpu":
                 print(f"Jacobi retries (n, attempt): {ptgen_gpu.RETRIES}", flush=True)
+                if ptgen_gpu._PHASES is not None:
+                    print(f"PHASES (s, synchronised): {ptgen_gpu._PHASES}", flush=True)
             print(f"RESULT {name} {side} tail={a.tail} K={K} steps={n_tot} {el:.2f} s "
                   f"(whole PT {'measured' if n_tot == 2 * K else 'extrapolated'}: {full:.1f} s)", flush=True)
 
