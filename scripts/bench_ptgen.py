@@ -5,6 +5,7 @@ cases (QD phonons, ae 3 nm unless stated, T 4 K, bond cap 128 for N <= 4):
   bx05   biexciton at the reference's defaults (four_level_system/linear.py:8): dt 0.5, t_mem 20.48 -> K = 41, 1e-10
   tls    TLS at the reference's defaults (tls.py:16): dt 0.1, t_mem 6.4 -> K = 64, ae 5 nm, threshold 1e-8
   bx01   biexciton at dt 0.1 (the bench's step): K = 205, 1e-10
+  sx05   six-level at the reference's defaults (six_level_system/linear.py:28, 50, 67): dt 0.5, K = 41, 1e-10, bond cap 64
 usage: python scripts/bench_ptgen.py [--case bx05,tls,bx01] [--steps N] [--host] [--tail qrcp|svd]"""
 import argparse
 import os
@@ -18,6 +19,7 @@ CASES = {
     "bx05": dict(lam=[0, 1, 1, 2], dt=0.5, t_mem=20.48, ae=3.0, thr=1e-10),
     "tls": dict(lam=[0, 1], dt=0.1, t_mem=6.4, ae=5.0, thr=1e-8),
     "bx01": dict(lam=[0, 1, 1, 2], dt=0.1, t_mem=20.48, ae=3.0, thr=1e-10),
+    "sx05": dict(lam=[0, 1, 1, 1, 1, 2], dt=0.5, t_mem=20.48, ae=3.0, thr=1e-10, cap=64),
 }
 
 
@@ -41,11 +43,11 @@ def main():
         eta, delta = ptgen.eta_coefficients(J, 4.0, c["dt"], K)
         for side in (["gpu", "host"] if a.host else ["gpu"]):
             if side == "gpu":
-                b = ptgen_gpu.GaussianPTBuilderGPU(A, eta, delta, c["dt"], c["thr"], 128, tail=a.tail)
+                b = ptgen_gpu.GaussianPTBuilderGPU(A, eta, delta, c["dt"], c["thr"], c.get("cap", 128), tail=a.tail)
                 import torch
                 sync = torch.cuda.synchronize
             else:
-                b = ptgen.GaussianPTBuilder(A, eta, delta, c["dt"], c["thr"], 128)
+                b = ptgen.GaussianPTBuilder(A, eta, delta, c["dt"], c["thr"], c.get("cap", 128))
                 sync = lambda: None  # noqa: E731
             n_tot = 2 * K if not a.steps else min(a.steps, 2 * K)
             t0 = time.perf_counter()
