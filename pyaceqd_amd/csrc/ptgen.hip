@@ -1224,6 +1224,177 @@ __global__ __launch_bounds__(256) void jac_persist_kernel(JacArgs a, JacPersist 
     if (blockIdx.x == 0 && tid == 0) *q.sweeps = sweep;
 }
 
+// block one-sided Jacobi, persistent: columns dealt into blocks of JB = 4; workgroup i takes block pair i of a
+// round-robin tournament over the blocks each round, loads the pair's 2 JB columns of X and V into LDS (every load of
+// a wave in flight at once), runs one inner sweep over the 2 JB (2 JB - 1) / 2 local pairs (2 JB - 1 sub-rounds, one
+// wave per pair, each rotation on register copies of its four column slices), stores the columns back and meets the
+// grid at jac_persist_kernel's barrier (16-B sc1 accesses, one counter add per workgroup, bounded polls). A sweep is
+// ceil(n / JB) - 1 grid barriers instead of n - 1. Stops at the first sweep without a rotation. LDS 4 JB n complex.
+constexpr int JB = 4;
+
+template <int EPL>
+__device__ __forceinline__ bool jac_rotate_regs(double2* xp, double2* xq, double2* vp, double2* vq, int n, double tol,
+                                                double zero2, int lane) {
+    double2 up[EPL], uq[EPL], wp[EPL], wq[EPL];
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) {
+        const int r = lane + 64 * e;
+        const bool in = r < n;
+        up[e] = in ? xp[r] : c_zero();
+        uq[e] = in ? xq[r] : c_zero();
+        wp[e] = in ? vp[r] : c_zero();
+        wq[e] = in ? vq[r] : c_zero();
+    }
+    double sa = 0.0, sb = 0.0;
+    double2 c = c_zero();
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) {
+        sa += c_abs2(up[e]);
+        sb += c_abs2(uq[e]);
+        c.x += up[e].x * uq[e].x + up[e].y * uq[e].y;
+        c.y += up[e].x * uq[e].y - up[e].y * uq[e].x;
+    }
+    sa = wsum(sa);
+    sb = wsum(sb);
+    c = wsum2(c);
+    const double ac = sqrt(c.x * c.x + c.y * c.y);
+    if (sa < zero2 || sb < zero2) return false;
+    if (!(ac > tol * sqrt(sa * sb)) || ac == 0.0) return false;
+    const double2 eph = make_double2(c.x / ac, -c.y / ac);
+    const double zeta = (sb - sa) / (2.0 * ac);
+    const double tt = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+    const double cs = 1.0 / sqrt(1.0 + tt * tt), sn = cs * tt;
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) {
+        const int r = lane + 64 * e;
+        if (r >= n) continue;
+        const double2 u = up[e], w = c_mul(uq[e], eph);
+        xp[r] = make_double2(cs * u.x - sn * w.x, cs * u.y - sn * w.y);
+        xq[r] = make_double2(sn * u.x + cs * w.x, sn * u.y + cs * w.y);
+        const double2 u2 = wp[e], w2 = c_mul(wq[e], eph);
+        vp[r] = make_double2(cs * u2.x - sn * w2.x, cs * u2.y - sn * w2.y);
+        vq[r] = make_double2(sn * u2.x + cs * w2.x, sn * u2.y + cs * w2.y);
+    }
+    return true;
+}
+
+template <int EPL>
+__global__ __launch_bounds__(256) void jac_block_kernel(JacArgs a, JacPersist q, int nblk) {
+    extern __shared__ double2 sm[];  // X columns [2 JB][n], then V columns [2 JB][n]
+    __shared__ int s_rot, s_abort, s_done;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n = a.n;
+    const unsigned G = gridDim.x;
+    const double zero2 = *a.zero2;
+    const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(a.X, 0, n * n * 16, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rV = __builtin_amdgcn_make_buffer_rsrc(a.V, 0, n * n * 16, 0x00020000);
+    double2* sX = sm;
+    double2* sV = sm + 2 * JB * n;
+    unsigned epoch = 0;
+    int sweep = 0;
+    if (tid == 0) s_abort = 0;
+    for (; sweep < q.max_sweeps; ++sweep) {
+        if (tid == 0) s_rot = 0;
+        __syncthreads();
+        for (int t = 0; t < nblk - 1; ++t) {
+            int bp, bq;
+            jac_pair(t, blockIdx.x, nblk, bp, bq);
+            // wave w owns local columns w and w + 4 for the load and the store
+            int gcs[2];
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) {
+                const int c = wave + 4 * cc;
+                gcs[cc] = c < JB ? bp * JB + c : bq * JB + (c - JB);
+            }
+            {
+                double2 rx[2][EPL], rv[2][EPL];
+#pragma unroll
+                for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+                    for (int e = 0; e < EPL; ++e) {
+                        const int r = lane + 64 * e;
+                        const bool in = gcs[cc] < n && r < n;
+                        rx[cc][e] = in ? ld16(rX, gcs[cc] * n + r) : c_zero();
+                        rv[cc][e] = in ? ld16(rV, gcs[cc] * n + r) : c_zero();
+                    }
+#pragma unroll
+                for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+                    for (int e = 0; e < EPL; ++e) {
+                        const int r = lane + 64 * e;
+                        if (r < n) {
+                            sX[(wave + 4 * cc) * n + r] = rx[cc][e];
+                            sV[(wave + 4 * cc) * n + r] = rv[cc][e];
+                        }
+                    }
+            }
+            __syncthreads();
+            for (int st = 0; st < 2 * JB - 1; ++st) {  // inner sweep: wave w rotates local pair w of sub-round st
+                int lp, lq;
+                jac_pair(st, wave, 2 * JB, lp, lq);
+                const int gp = lp < JB ? bp * JB + lp : bq * JB + (lp - JB);
+                const int gq = lq < JB ? bp * JB + lq : bq * JB + (lq - JB);
+                if (gp < n && gq < n) {
+                    const bool rot = jac_rotate_regs<EPL>(sX + lp * n, sX + lq * n, sV + lp * n, sV + lq * n, n, a.tol,
+                                                          zero2, lane);
+                    if (rot && lane == 0) atomicAdd(&s_rot, 1);
+                }
+                __syncthreads();
+            }
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) {
+                if (gcs[cc] >= n) continue;
+                double2 rx[EPL], rv[EPL];
+#pragma unroll
+                for (int e = 0; e < EPL; ++e) {
+                    const int r = lane + 64 * e;
+                    rx[e] = r < n ? sX[(wave + 4 * cc) * n + r] : c_zero();
+                    rv[e] = r < n ? sV[(wave + 4 * cc) * n + r] : c_zero();
+                }
+#pragma unroll
+                for (int e = 0; e < EPL; ++e) {
+                    const int r = lane + 64 * e;
+                    if (r < n) {
+                        st16(rX, gcs[cc] * n + r, rx[e]);
+                        st16(rV, gcs[cc] * n + r, rv[e]);
+                    }
+                }
+            }
+            // ---- grid barrier (and, after a sweep's last round, the sweep's rotation count)
+            ++epoch;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) {
+                if (t == nblk - 2 && s_rot)
+                    __hip_atomic_fetch_add((gu32*)(q.cnt + sweep), (unsigned)s_rot, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_fetch_add((gu32*)q.bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (tid < 64) {
+                const unsigned target = G * epoch;
+                unsigned spins = 0;
+                bool ok = true;
+                while (__hip_atomic_load((gu32*)q.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > q.spin_limit) { ok = false; break; }
+                }
+                if (tid == 0 && !ok) {
+                    s_abort = 1;
+                    __hip_atomic_store((gu32*)q.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            __syncthreads();
+            if (s_abort) return;
+        }
+        if (tid == 0)
+            s_done = __hip_atomic_load((gu32*)(q.cnt + sweep), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+        __syncthreads();
+        if (s_done) { ++sweep; break; }
+    }
+    if (blockIdx.x == 0 && tid == 0) *q.sweeps = sweep;
+}
+
 // sigma_j = |x_j|, x_j <- x_j / sigma_j (zero columns stay zero)
 __global__ void jac_finish_kernel(double2* X, int n, double* sigma) {
     const int lane = threadIdx.x & 63;
@@ -1563,7 +1734,29 @@ extern "C" int pqd_ptg_jacobi(void* stream, pqd_c128* Xp, int32_t n, pqd_c128* V
             q.spin_limit = 1u << 22;
             PCHK(hipMemsetAsync(cnt + 16, 0, (64 + 200) * sizeof(int) - 16 * sizeof(int), s));
             const dim3 g((npair + wpb - 1) / wpb), b(64 * wpb);
-            switch (epl) {
+            int nblk = (n + JB - 1) / JB;
+            nblk += nblk & 1;  // even: the round-robin pairs every block each round (a block past n is all dummies)
+            const size_t lds_blk = (size_t)4 * JB * n * sizeof(double2);
+            constexpr int JB_LDS_MAX = 160 * 1024 - 256;  // the kernel's own static LDS words come on top
+            // PQD_PTG_JBLOCK=0: the column-pair kernel (one grid barrier per tournament round of single columns)
+            const bool jblock = env_int("PQD_PTG_JBLOCK", 1) != 0 && epl <= 8 && lds_blk <= (size_t)JB_LDS_MAX &&
+                                nblk >= 2;
+            if (jblock) {
+                static bool attr = false;
+                if (!attr) {
+                    for (const void* f : {(const void*)jac_block_kernel<1>, (const void*)jac_block_kernel<2>,
+                                          (const void*)jac_block_kernel<4>, (const void*)jac_block_kernel<8>})
+                        PCHK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, JB_LDS_MAX));
+                    attr = true;
+                }
+                const dim3 gb(nblk / 2);
+                switch (epl) {
+                    case 1: hipLaunchKernelGGL(jac_block_kernel<1>, gb, b, lds_blk, s, a, q, nblk); break;
+                    case 2: hipLaunchKernelGGL(jac_block_kernel<2>, gb, b, lds_blk, s, a, q, nblk); break;
+                    case 4: hipLaunchKernelGGL(jac_block_kernel<4>, gb, b, lds_blk, s, a, q, nblk); break;
+                    default: hipLaunchKernelGGL(jac_block_kernel<8>, gb, b, lds_blk, s, a, q, nblk); break;
+                }
+            } else switch (epl) {
                 case 1: hipLaunchKernelGGL(jac_persist_kernel<1>, g, b, 0, s, a, q); break;
                 case 2: hipLaunchKernelGGL(jac_persist_kernel<2>, g, b, 0, s, a, q); break;
                 case 4: hipLaunchKernelGGL(jac_persist_kernel<4>, g, b, 0, s, a, q); break;

@@ -144,18 +144,20 @@ def test_ptg_qrcp_rank_revealing(monkeypatch, small, m, n, rank):
     assert np.linalg.norm(W - Q2 @ R2) <= np.sqrt(n - k + 1) * tol * 1.01 + 1e-13 * np.linalg.norm(W)
 
 
-@pytest.mark.parametrize("small", ["1", "0", "0-rounds"])
+@pytest.mark.parametrize("small", ["1", "0", "0-persist", "0-rounds"])
 @pytest.mark.parametrize("r,c,graded", [(6, 9, False), (40, 200, True), (384, 1350, False), (300, 90, True),
                                          (120, 120, True), (45, 101, "lowrank"), (201, 700, "lowrank"),
                                          (1100, 700, True)])
 def test_ptg_svd_matches_lapack(monkeypatch, small, r, c, graded):
     """thin SVD vs LAPACK on random, graded (1 .. 1e-13) and numerically low-rank blocks (odd sizes: the Jacobi
     tournament's dummy player; rank 1/4: three quarters of the columns at the rounding floor, as the stacked
-    generator blocks are). Jacobi on the single-workgroup kernel, the persistent grid kernel (n <= 1024, default)
-    and one launch per round ("0-rounds", also what n > 1024 uses)"""
+    generator blocks are). Jacobi on the single-workgroup kernel, the persistent block kernel (two 4-column blocks per
+    workgroup, n <= 512, default), the persistent column-pair kernel ("0-persist", n <= 1024) and one launch per round
+    ("0-rounds", also what n > 1024 uses)"""
     from pyaceqd_amd import ptgen_gpu
     monkeypatch.setenv("PQD_PTG_SMALL", small[0])
     monkeypatch.setenv("PQD_PTG_JPERSIST", "0" if small == "0-rounds" else "1")
+    monkeypatch.setenv("PQD_PTG_JBLOCK", "0" if small in ("0-rounds", "0-persist") else "1")
     rng = np.random.default_rng(r * 7 + c)
     k = min(r, c)
     if graded == "lowrank":
