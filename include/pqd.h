@@ -284,6 +284,10 @@ int pqd_ptg_qr(void* stream, pqd_c128* W, int32_t m, int32_t n, int32_t pivot, d
  * zero (never rotated). Outputs: X <- U (unit columns, unsorted), V (n x n), sigma (n, unsorted), *sweeps (host). */
 int pqd_ptg_jacobi(void* stream, pqd_c128* X, int32_t n, pqd_c128* V, double* sigma, double tol, double zero_tol,
                    int32_t max_sweeps, int32_t* sweeps);
+/* pqd_ptg_jacobi runs its sweeps in one persistent launch (a grid barrier per round) when n <= 1024; if a barrier
+ * wait times out (the workgroups were not all resident), the launch is rerun from a saved copy of X with one launch
+ * per round. pqd_ptg_counters: how many times that happened in this process (diagnostics, tests). */
+int pqd_ptg_counters(int32_t* jacobi_fallbacks);
 
 #ifdef __cplusplus
 }

@@ -28,6 +28,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -1426,6 +1427,8 @@ int perr(int code, const char* msg) {
         }                                                                                        \
     } while (0)
 
+std::atomic<int> g_jac_fallbacks{0};  // persistent Jacobi launches rerun per round (barrier timeout)
+
 // per-process scratch (the generator runs one factorization at a time per stream; guarded for safety)
 std::mutex g_mu;
 struct Scratch {
@@ -1695,6 +1698,12 @@ extern "C" int pqd_ptg_qr(void* stream, pqd_c128* Wp, int32_t m, int32_t n, int3
     return PQD_OK;
 }
 
+extern "C" int pqd_ptg_counters(int32_t* jacobi_fallbacks) {
+    if (!jacobi_fallbacks) return perr(PQD_ERR_ARG, "pqd_ptg_counters: NULL argument");
+    *jacobi_fallbacks = g_jac_fallbacks.load();
+    return PQD_OK;
+}
+
 extern "C" int pqd_ptg_jacobi(void* stream, pqd_c128* Xp, int32_t n, pqd_c128* Vp, double* sigma, double tol,
                               double zero_tol, int32_t max_sweeps, int32_t* sweeps_out) {
     if (!Xp || !Vp || !sigma || !sweeps_out) return perr(PQD_ERR_ARG, "pqd_ptg_jacobi: NULL argument");
@@ -1704,8 +1713,12 @@ extern "C" int pqd_ptg_jacobi(void* stream, pqd_c128* Xp, int32_t n, pqd_c128* V
     double2* X = reinterpret_cast<double2*>(Xp);
     double2* V = reinterpret_cast<double2*>(Vp);
     void* base = nullptr;
-    PCHK(scratch(al((64 + 200) * sizeof(int)), &base));
+    // counters, then a copy of X: a persistent launch whose grid barrier times out (workgroups not co-resident, e.g.
+    // under contention from other work on the device) is rerun from this copy with one launch per round
+    const size_t b_cnt = al((64 + 200) * sizeof(int));
+    PCHK(scratch(b_cnt + al((size_t)n * n * sizeof(double2)), &base));
     int* cnt = static_cast<int*>(base);
+    double2* Xbak = reinterpret_cast<double2*>(static_cast<char*>(base) + b_cnt);
     double* zero2 = reinterpret_cast<double*>(cnt + 8);
     int sweeps = 0;
     // zero threshold relative to the Frobenius norm (rotation-invariant): |x_j| < zero_tol * ||X||_F
@@ -1724,14 +1737,16 @@ extern "C" int pqd_ptg_jacobi(void* stream, pqd_c128* Xp, int32_t n, pqd_c128* V
         hipLaunchKernelGGL(jac_init_kernel, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, s, V, n);
         const int npair = a.nn / 2, wpb = 4;
         const int epl = n <= 64 ? 1 : n <= 128 ? 2 : n <= 256 ? 4 : n <= 512 ? 8 : n <= 1024 ? 16 : 0;
-        if (epl && env_int("PQD_PTG_JPERSIST", 1) != 0 && max_sweeps <= 200) {
+        bool persist = epl && env_int("PQD_PTG_JPERSIST", 1) != 0 && max_sweeps <= 200;
+        if (persist) {
+            PCHK(hipMemcpyAsync(Xbak, X, nv * sizeof(double2), hipMemcpyDeviceToDevice, s));
             JacPersist q;
             q.bar = reinterpret_cast<unsigned*>(cnt + 16);
             q.err = reinterpret_cast<unsigned*>(cnt + 32);
             q.sweeps = cnt + 48;
             q.cnt = cnt + 64;
             q.max_sweeps = max_sweeps;
-            q.spin_limit = 1u << 22;
+            q.spin_limit = (unsigned)env_int("PQD_PTG_JSPIN", 1 << 22);  // polls per barrier wait (tests: 1)
             PCHK(hipMemsetAsync(cnt + 16, 0, (64 + 200) * sizeof(int) - 16 * sizeof(int), s));
             const dim3 g((npair + wpb - 1) / wpb), b(64 * wpb);
             int nblk = (n + JB - 1) / JB;
@@ -1768,9 +1783,16 @@ extern "C" int pqd_ptg_jacobi(void* stream, pqd_c128* Xp, int32_t n, pqd_c128* V
             PCHK(hipMemcpyAsync(&h[0], q.sweeps, sizeof(int), hipMemcpyDeviceToHost, s));
             PCHK(hipMemcpyAsync(&h[1], q.err, sizeof(int), hipMemcpyDeviceToHost, s));
             PCHK(hipStreamSynchronize(s));
-            if (h[1]) return perr(PQD_ERR_HIP, "pqd_ptg_jacobi: a grid barrier of the persistent kernel timed out");
-            sweeps = h[0];
-        } else {
+            if (h[1]) {  // a barrier wait timed out: every workgroup has left; start over from X, one launch per round
+                PCHK(hipMemcpyAsync(X, Xbak, nv * sizeof(double2), hipMemcpyDeviceToDevice, s));
+                hipLaunchKernelGGL(jac_init_kernel, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, s, V, n);
+                persist = false;
+                g_jac_fallbacks.fetch_add(1);
+            } else {
+                sweeps = h[0];
+            }
+        }
+        if (!persist) {
             for (; sweeps < max_sweeps;) {
                 PCHK(hipMemsetAsync(cnt, 0, sizeof(int), s));
                 for (int t = 0; t < a.nn - 1; ++t)

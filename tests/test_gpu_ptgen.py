@@ -144,7 +144,7 @@ def test_ptg_qrcp_rank_revealing(monkeypatch, small, m, n, rank):
     assert np.linalg.norm(W - Q2 @ R2) <= np.sqrt(n - k + 1) * tol * 1.01 + 1e-13 * np.linalg.norm(W)
 
 
-@pytest.mark.parametrize("small", ["1", "0", "0-persist", "0-rounds"])
+@pytest.mark.parametrize("small", ["1", "0", "0-persist", "0-rounds", "0-timeout"])
 @pytest.mark.parametrize("r,c,graded", [(6, 9, False), (40, 200, True), (384, 1350, False), (300, 90, True),
                                          (120, 120, True), (45, 101, "lowrank"), (201, 700, "lowrank"),
                                          (1100, 700, True)])
@@ -152,12 +152,15 @@ def test_ptg_svd_matches_lapack(monkeypatch, small, r, c, graded):
     """thin SVD vs LAPACK on random, graded (1 .. 1e-13) and numerically low-rank blocks (odd sizes: the Jacobi
     tournament's dummy player; rank 1/4: three quarters of the columns at the rounding floor, as the stacked
     generator blocks are). Jacobi on the single-workgroup kernel, the persistent block kernel (two 4-column blocks per
-    workgroup, n <= 512, default), the persistent column-pair kernel ("0-persist", n <= 1024) and one launch per round
-    ("0-rounds", also what n > 1024 uses)"""
+    workgroup, n <= 512, default), the persistent column-pair kernel ("0-persist", n <= 1024), one launch per round
+    ("0-rounds", also what n > 1024 uses), and a persistent launch whose grid barrier times out and is rerun per round
+    from a copy of X ("0-timeout")"""
     from pyaceqd_amd import ptgen_gpu
     monkeypatch.setenv("PQD_PTG_SMALL", small[0])
     monkeypatch.setenv("PQD_PTG_JPERSIST", "0" if small == "0-rounds" else "1")
     monkeypatch.setenv("PQD_PTG_JBLOCK", "0" if small in ("0-rounds", "0-persist") else "1")
+    # 0-timeout: one poll per barrier wait, so the persistent launch times out and is rerun per round from a copy
+    monkeypatch.setenv("PQD_PTG_JSPIN", "1" if small == "0-timeout" else str(1 << 22))
     rng = np.random.default_rng(r * 7 + c)
     k = min(r, c)
     if graded == "lowrank":
@@ -168,7 +171,18 @@ def test_ptg_svd_matches_lapack(monkeypatch, small, r, c, graded):
         A = (U0 * np.logspace(0, -13, k)[None, :]) @ V0.conj().T
     else:
         A = _rand(rng, r, c)
-    U, S, Vh = (x.cpu().numpy() for x in ptgen_gpu.svd(_dev(A)))
+    import ctypes
+    from pyaceqd_amd import _lib
+    dA = _dev(A)                                   # the device (torch's HIP runtime) before the library's first call
+    fb0 = ctypes.c_int32(0)
+    _lib.check(_lib.lib().pqd_ptg_counters(ctypes.byref(fb0)))
+    U, S, Vh = (x.cpu().numpy() for x in ptgen_gpu.svd(dA))
+    fb1 = ctypes.c_int32(0)
+    _lib.check(_lib.lib().pqd_ptg_counters(ctypes.byref(fb1)))
+    if small == "0-timeout" and min(r, c) >= 64:  # several workgroups: the fallback ran
+        assert fb1.value > fb0.value
+    elif small != "0-timeout":
+        assert fb1.value == fb0.value
     Sn = np.linalg.svd(A, compute_uv=False)
     kk = len(S)                                    # the numerical rank at 1e-14 (the rest is dropped)
     assert np.max(np.abs(S - Sn[:kk])) < 1e-13 * Sn[0]
