@@ -127,6 +127,7 @@ _SIGS = {
     "pqd_ptg_jacobi": ([C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_double, C.c_double,
                         C.c_int32, P_I32], C.c_int),
     "pqd_ptg_counters": ([P_I32], C.c_int),
+    "pqd_ptg_qr_counters": ([P_I32], C.c_int),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -1396,6 +1396,161 @@ __global__ __launch_bounds__(256) void jac_block_kernel(JacArgs a, JacPersist q,
     if (blockIdx.x == 0 && tid == 0) *q.sweeps = sweep;
 }
 
+// persistent column-pivoted QR: every step in ONE launch, qr_step_wg_kernel's arithmetic. Workgroup g owns PHYSICAL
+// column g for the whole factorization and holds it in registers; the permutation lives in each workgroup's LDS (every
+// workgroup makes the same swap). Step k: the pivot search over the trailing norms (sc1 loads, the same scan and tie
+// rule as the launch path), the stop test, the swap; the pivot column's owner records the reflector, the trailing
+// workgroups read the pivot column (16-B sc1 loads), update their column in registers, store its rows >= k (sc1,
+// for a later pivot read and for R) and its trailing norm, then the grid meets at jac_persist_kernel's barrier.
+// Workgroups whose column is eliminated only keep the barrier count. Results equal the launch path's bit for bit.
+// Needs all n workgroups co-resident (the host checks the occupancy; a timed-out barrier wait sets *q.err and every
+// workgroup leaves, and the host reruns the factorization one launch per step from a saved copy).
+struct QRPersist {
+    unsigned* bar;
+    unsigned* err;
+    unsigned spin_limit;
+};
+template <int EPT>
+__global__ __launch_bounds__(WG_T) void qrcp_persist_kernel(QRArgs a, QRPersist q) {
+    extern __shared__ int s_perm[];  // n
+    __shared__ double red[2][4 * 3];
+    __shared__ int s_p, s_abort;
+    __shared__ double s_best;
+    __shared__ double2 s_ck;
+    const int tid = threadIdx.x, g = blockIdx.x, m = a.m, n = a.n;
+    const unsigned G = gridDim.x;
+    const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(a.W, 0, m * n * 16, 0x00020000);
+    for (int j = tid; j < n; j += WG_T) s_perm[j] = j;
+    if (tid == 0) s_abort = 0;
+    double2 cj[EPT];
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+        const int i = tid + WG_T * e;
+        cj[e] = i < m ? a.W[(size_t)g * m + i] : c_zero();
+    }
+    bool done = false;  // this column is a reflector column (eliminated)
+    double lim = a.tol2;
+    int k = 0;
+    unsigned epoch = 0;
+    __syncthreads();
+    for (; k < a.kmax; ++k) {
+        const double* nin = a.norms + (size_t)(k & 1) * n;
+        double* nout = a.norms + (size_t)((k + 1) & 1) * n;
+        if (tid < 64) {
+            double best = -1.0;
+            int bj = k;
+            for (int jj = k + tid; jj < n; jj += 64) {
+                const unsigned long long b = __hip_atomic_load((gu64*)(nin + s_perm[jj]), __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT);
+                const double v = __longlong_as_double((long long)b);
+                if (v > best) { best = v; bj = jj; }
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const double ob = __shfl_xor(best, o);
+                const int oj = __shfl_xor(bj, o);
+                if (ob > best || (ob == best && oj < bj)) { best = ob; bj = oj; }
+            }
+            if (tid == 0) { s_p = bj; s_best = best; }
+        }
+        __syncthreads();
+        const int p = s_p;
+        const double sb = s_best;
+        if (a.rel2 > 0.0 && k == 0) {
+            lim = a.rel2 * sb;
+            if (g == 0 && tid == 0) *a.thr = lim;
+        }
+        if (sb <= lim) {
+            if (g == 0 && tid == 0) a.ctrl[0] = k;
+            break;
+        }
+        const int cp = s_perm[p];  // the pivot's physical column
+        __syncthreads();           // every thread has read s_perm[p] before the swap
+        if (tid == 0) { s_perm[p] = s_perm[k]; s_perm[k] = cp; }
+        if (!done) {
+            const bool own = cp == g;  // this workgroup's column is the pivot: it records the reflector
+            // row k of this column (own: alpha; trailing: c_k) to every thread through LDS (ordered by wg_reduce's
+            // barrier); the trailing workgroups read the pivot column's rows >= k
+#pragma unroll
+            for (int e = 0; e < EPT; ++e)
+                if (tid + WG_T * e == k) s_ck = cj[e];
+            double2 u[EPT];
+#pragma unroll
+            for (int e = 0; e < EPT; ++e) {
+                const int i = tid + WG_T * e;
+                u[e] = own ? cj[e] : ((i > k && i < m) ? ld16(rW, cp * m + i) : c_zero());
+            }
+            const double2 alpha_g = own ? c_zero() : ld16(rW, cp * m + k);
+            double r1[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+            for (int e = 0; e < EPT; ++e) {
+                const int i = tid + WG_T * e;
+                if (i > k && i < m) {
+                    const double2 v = u[e], w = own ? c_zero() : cj[e];
+                    r1[0] += c_abs2(v);
+                    r1[1] += v.x * w.x + v.y * w.y;
+                    r1[2] += v.x * w.y - v.y * w.x;
+                }
+            }
+            wg_reduce<3>(r1, red[0]);
+            const Refl R = make_refl(own ? s_ck : alpha_g, r1[0]);
+            if (own) {
+                if (tid == 0) { a.tau[k] = R.tau; a.scale[k] = R.scale; a.beta[k] = R.beta; }
+                done = true;
+            } else {
+                const double2 ck = s_ck;
+                const double2 sv = c_add(ck, c_cmul(R.scale, make_double2(r1[1], r1[2])));
+                const double2 ct = c_cmul(R.tau, sv);
+                const double2 f = c_mul(ct, R.scale);  // c_i -= ct v_i = f x_i for i > k
+                double r2[1] = {0.0};
+#pragma unroll
+                for (int e = 0; e < EPT; ++e) {
+                    const int i = tid + WG_T * e;
+                    if (i > k && i < m) {
+                        const double2 ci = c_sub(cj[e], c_mul(f, u[e]));
+                        cj[e] = ci;
+                        st16(rW, g * m + i, ci);
+                        r2[0] += c_abs2(ci);
+                    } else if (i == k) {
+                        cj[e] = c_sub(ck, ct);
+                        st16(rW, g * m + k, cj[e]);
+                    }
+                }
+                wg_reduce<1>(r2, red[1]);
+                if (tid == 0)
+                    __hip_atomic_store((gu64*)(nout + g), (unsigned long long)__double_as_longlong(r2[0]),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        // ---- grid barrier
+        ++epoch;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_fetch_add((gu32*)q.bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (tid < 64) {
+            const unsigned target = G * epoch;
+            unsigned spins = 0;
+            bool ok = true;
+            while (__hip_atomic_load((gu32*)q.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > q.spin_limit) { ok = false; break; }
+            }
+            if (tid == 0 && !ok) {
+                s_abort = 1;
+                __hip_atomic_store((gu32*)q.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __syncthreads();
+        if (s_abort) return;
+    }
+    // the final permutation where the launch path leaves it (the buffer of parity rank & 1)
+    if (g == 0)
+        for (int j = tid; j < n; j += WG_T) a.perm[(size_t)(k & 1) * n + j] = s_perm[j];
+}
+
 // sigma_j = |x_j|, x_j <- x_j / sigma_j (zero columns stay zero)
 __global__ void jac_finish_kernel(double2* X, int n, double* sigma) {
     const int lane = threadIdx.x & 63;
@@ -1428,6 +1583,7 @@ int perr(int code, const char* msg) {
     } while (0)
 
 std::atomic<int> g_jac_fallbacks{0};  // persistent Jacobi launches rerun per round (barrier timeout)
+std::atomic<int> g_qr_fallbacks{0};   // persistent QRCP launches rerun one launch per step (barrier timeout)
 
 // per-process scratch (the generator runs one factorization at a time per stream; guarded for safety)
 std::mutex g_mu;
@@ -1503,6 +1659,36 @@ void launch_step_wg(int ept, const QRArgs& a, int k, int grid, hipStream_t s) {
         case 8: hipLaunchKernelGGL(qr_step_wg_kernel<8>, dim3(grid), dim3(WG_T), 0, s, a, k); break;
         default: hipLaunchKernelGGL(qr_step_wg_kernel<16>, dim3(grid), dim3(WG_T), 0, s, a, k); break;
     }
+}
+
+// the persistent QRCP kernel for ept, and whether its n workgroups (256 threads, n ints of LDS) can all be resident
+const void* qrcp_persist_fn(int ept) {
+    switch (ept) {
+        case 1: return (const void*)qrcp_persist_kernel<1>;
+        case 2: return (const void*)qrcp_persist_kernel<2>;
+        case 4: return (const void*)qrcp_persist_kernel<4>;
+        case 8: return (const void*)qrcp_persist_kernel<8>;
+        default: return (const void*)qrcp_persist_kernel<16>;
+    }
+}
+bool qrcp_persist_fits(int ept, int n) {
+    static int cus = 0;
+    static int per_cu[17] = {0};
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return false;
+    }
+    if (!per_cu[ept]) {
+        int nb = 0;
+        // LDS: the permutation (n ints) at the largest n taken (4096), so the answer holds for every n below it
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, qrcp_persist_fn(ept), WG_T, 4096 * sizeof(int)) !=
+            hipSuccess)
+            return false;
+        per_cu[ept] = nb > 0 ? nb : -1;
+    }
+    return n <= 4096 && per_cu[ept] > 0 && (long long)per_cu[ept] * cus >= n;
 }
 
 // column steps k .. k_end-1 of a (updating logical columns < a.n): pairs on plain QRs, workgroup-per-column kernels
@@ -1601,12 +1787,17 @@ extern "C" int pqd_ptg_qr(void* stream, pqd_c128* Wp, int32_t m, int32_t n, int3
     const bool blocked = !pivot && !small && m >= n && n > QB &&
                          (blk_env == 1 || (blk_env < 0 && (size_t)m * n >= (size_t)1000000));
     const bool qfb = !small && env_int("PQD_PTG_QFB", 1) != 0;
+    // column-pivoted QRs whose columns fit in registers: every step in one persistent launch (PQD_PTG_QPERSIST=1;
+    // default: one launch per step)
+    const bool qpersist = pivot && !small && ept > 0 && kmax >= 2 && env_int("PQD_PTG_QPERSIST", 0) != 0 &&
+                          qrcp_persist_fits(ept, n);
     const bool sepx = pairs || blocked;  // reflector columns in their own buffer X
     const size_t b_tau = al(kmax * sizeof(double2)), b_beta = al(kmax * sizeof(double)),
                  b_perm = al(2 * (size_t)n * sizeof(int)), b_norm = al(2 * (size_t)n * sizeof(double)),
                  b_ctrl = al(64 * sizeof(int)), b_x = sepx ? al((size_t)m * kmax * sizeof(double2)) : 0,
-                 b_blk = (blocked || qfb) ? block_bytes(m, n) : 0;
-    PCHK(scratch(2 * b_tau + b_beta + b_perm + b_norm + b_ctrl + b_x + b_blk, &base));
+                 b_blk = (blocked || qfb) ? block_bytes(m, n) : 0,
+                 b_bak = qpersist ? al((size_t)m * n * sizeof(double2)) : 0;
+    PCHK(scratch(2 * b_tau + b_beta + b_perm + b_norm + b_ctrl + b_x + b_blk + b_bak, &base));
     char* c = static_cast<char*>(base);
     QRArgs a;
     a.W = W; a.m = m; a.n = n; a.kmax = kmax; a.pivot = pivot ? 1 : 0; a.tol2 = tol2; a.rel2 = rel2;
@@ -1620,6 +1811,8 @@ extern "C" int pqd_ptg_qr(void* stream, pqd_c128* Wp, int32_t m, int32_t n, int3
     c += b_x;
     BlockBufs bb{};
     if (b_blk) bb = carve_block(c, m, n);
+    double2* Wbak = b_bak ? reinterpret_cast<double2*>(c) : nullptr;  // after the blocks: carve_block advanced c
+    c += b_bak;
     int* d_rank = a.ctrl + 8;
     a.thr = reinterpret_cast<double*>(a.ctrl + 16);
     if (small) {
@@ -1661,6 +1854,31 @@ extern "C" int pqd_ptg_qr(void* stream, pqd_c128* Wp, int32_t m, int32_t n, int3
                 block_apply(W + (size_t)(k0 + nb) * m + k0, m, n - k0 - nb, m - k0, k0, nb, 1, a.tau, bb, s);
             }
         }
+    } else if (qpersist) {
+        QRPersist q;
+        q.bar = reinterpret_cast<unsigned*>(a.ctrl + 32);
+        q.err = reinterpret_cast<unsigned*>(a.ctrl + 40);
+        q.spin_limit = (unsigned)env_int("PQD_PTG_QSPIN", 1 << 22);  // polls per barrier wait (tests: 1)
+        PCHK(hipMemsetAsync(a.ctrl + 32, 0, 16 * sizeof(int), s));
+        PCHK(hipMemcpyAsync(Wbak, W, (size_t)m * n * sizeof(double2), hipMemcpyDeviceToDevice, s));
+        const size_t lds = (size_t)n * sizeof(int);
+        switch (ept) {
+            case 1: hipLaunchKernelGGL(qrcp_persist_kernel<1>, dim3(n), dim3(WG_T), lds, s, a, q); break;
+            case 2: hipLaunchKernelGGL(qrcp_persist_kernel<2>, dim3(n), dim3(WG_T), lds, s, a, q); break;
+            case 4: hipLaunchKernelGGL(qrcp_persist_kernel<4>, dim3(n), dim3(WG_T), lds, s, a, q); break;
+            case 8: hipLaunchKernelGGL(qrcp_persist_kernel<8>, dim3(n), dim3(WG_T), lds, s, a, q); break;
+            default: hipLaunchKernelGGL(qrcp_persist_kernel<16>, dim3(n), dim3(WG_T), lds, s, a, q); break;
+        }
+        PCHK(hipGetLastError());
+        unsigned e = 0;
+        PCHK(hipMemcpyAsync(&e, q.err, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+        PCHK(hipStreamSynchronize(s));
+        if (e) {  // a barrier wait timed out: every workgroup has left; start over from the copy, one launch per step
+            PCHK(hipMemcpyAsync(W, Wbak, (size_t)m * n * sizeof(double2), hipMemcpyDeviceToDevice, s));
+            hipLaunchKernelGGL(qr_init_kernel, dim3((n + wpb - 1) / wpb), dim3(64 * wpb), 0, s, a);
+            column_steps(a, 0, kmax, false, ept, s);
+            g_qr_fallbacks.fetch_add(1);
+        }
     } else {
         column_steps(a, 0, kmax, pairs, ept, s);
     }
@@ -1701,6 +1919,12 @@ extern "C" int pqd_ptg_qr(void* stream, pqd_c128* Wp, int32_t m, int32_t n, int3
 extern "C" int pqd_ptg_counters(int32_t* jacobi_fallbacks) {
     if (!jacobi_fallbacks) return perr(PQD_ERR_ARG, "pqd_ptg_counters: NULL argument");
     *jacobi_fallbacks = g_jac_fallbacks.load();
+    return PQD_OK;
+}
+
+extern "C" int pqd_ptg_qr_counters(int32_t* qrcp_fallbacks) {
+    if (!qrcp_fallbacks) return perr(PQD_ERR_ARG, "pqd_ptg_qr_counters: NULL argument");
+    *qrcp_fallbacks = g_qr_fallbacks.load();
     return PQD_OK;
 }
 

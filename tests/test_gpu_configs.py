@@ -96,6 +96,65 @@ def test_config1_tls_rabi_1000_steps(monkeypatch, sampling):
     assert exc[0] > 0.9                            # a pi pulse: the dot is inverted, then decays
 
 
+def _exact_lindblad(H, lind, rho0, ops, ts):
+    """<op>(t) = tr(op exp(L t) rho0) for a time-independent Lindbladian (row-major vec, scipy expm): the exact
+    solution, independent of the oracle and of the engine's step structure"""
+    import scipy.linalg as sla
+    from pyaceqd_amd.constants import hbar
+    N = H.shape[0]
+    eye = np.eye(N)
+    L = -1j / hbar * (np.kron(H, eye) - np.kron(eye, H.T))
+    for Lk, g in lind:
+        LdL = Lk.conj().T @ Lk
+        L = L + g * (np.kron(Lk, Lk.conj()) - 0.5 * np.kron(LdL, eye) - 0.5 * np.kron(eye, LdL.T))
+    rows = []
+    for t in ts:
+        r = (sla.expm(L * t) @ rho0.reshape(-1)).reshape(N, N)
+        rows.append([np.trace(o @ r) for o in ops])
+    return np.array(rows).T
+
+
+@pytest.mark.parametrize("sampling", ["ace_file", "exact"])
+def test_cw_drive_matches_exact_lindblad_solution(sampling):
+    """No phonons and a constant (resonant CW) drive make the Lindbladian time independent, so the engine's symmetric
+    Trotter steps must reproduce exp(L t) exactly: the HIP path (driver -> free propagators -> sweep -> output table)
+    against scipy's matrix exponential at 1e-11 over 2,000 steps, two orders inside the north star's 1e-8 no-phonon
+    tolerance, with neither the CPU oracle nor the engine's own lowering in the reference. TLS (tls.py strings) and the
+    biexciton with both polarisation channels, fine-structure splitting and x-y coupling (linear.py strings, pinned
+    to the reference's param text by test_params_golden.py). The ACE-file drive quantises the samples to %.8f, so the
+    exact solution uses the quantised amplitudes (general_system.py:55-71)."""
+    from pyaceqd_amd.constants import hbar
+    from pyaceqd_amd.pulses import CWLaser
+    from pyaceqd_amd.two_level_system.tls import tls
+    from pyaceqd_amd.four_level_system.linear import biexciton, biexciton_ops
+    q = (lambda v: float("%.8f" % v)) if sampling == "ace_file" else (lambda v: v)
+    e0 = 0.3
+    a = tls(0, 200, CWLaser(e0), dt=0.1, lindblad=True, pulse_sampling=sampling)
+    assert a.shape == (5, 2001)
+    X = -0.5 * np.pi * hbar * np.array([[0, 0], [1, 0]], complex)
+    H = q(e0) * (X + X.conj().T)
+    ops = [opgrammar.to_matrix(o, 2) for o in ["|0><0|_2", "|1><1|_2", "|0><1|_2", "|1><0|_2"]]
+    idx = np.arange(0, 2001, 40)
+    ref = _exact_lindblad(H, [(np.array([[0, 1], [0, 0]], complex), 1 / 100)], np.diag([1.0, 0]).astype(complex),
+                          ops, a[0].real[idx])
+    assert np.max(np.abs(a[1:, idx] - ref)) < 1e-11
+    assert np.ptp(ref[1].real) > 0.5                   # Rabi oscillations, damped
+    px = np.cos(0.3)
+    so, _, lo, io, _ = biexciton_ops(lindblad=True, delta_xy=0.1, coupl_xy=0.02)
+    b = biexciton(0, 200, CWLaser(0.5, polar_x=px), dt=0.1, lindblad=True, delta_xy=0.1, coupl_xy=0.02,
+                  pulse_sampling=sampling)
+    H = sum(opgrammar.to_matrix(o, 4) for o in so)
+    for op, ch in io:
+        f = q(0.5 * (px if ch == "x" else np.sqrt(1 - px ** 2)))
+        Xc = -0.5 * np.pi * hbar * opgrammar.to_matrix(op, 4)
+        H = H + f * (Xc + Xc.conj().T)
+    lind = [(opgrammar.to_matrix(o, 4), g) for o, g in lo]
+    ops = [opgrammar.to_matrix("|%d><%d|_4" % (k, k), 4) for k in range(4)]
+    ref = _exact_lindblad(H, lind, np.diag([1.0, 0, 0, 0]).astype(complex), ops, b[0].real[idx])
+    assert np.max(np.abs(b[1:, idx] - ref)) < 1e-11
+    assert min(np.max(ref[k].real) for k in range(1, 4)) > 5e-3    # every level is reached (|3>: 0.008)
+
+
 # ------------------------------------------------------------------------------------------------ config 2
 def _c2(structured):
     bc = _configs()

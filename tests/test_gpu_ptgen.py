@@ -115,6 +115,50 @@ def test_ptg_qrcp_step_kernels(monkeypatch, wg, m, n, rank):
     assert k2 == k and np.array_equal(perm2.cpu().numpy()[:k], p[:k])
 
 
+@pytest.mark.parametrize("m,n,rank,tolmode", [(1205, 300, 120, "abs"), (400, 250, None, "abs"), (3000, 200, None, "rel"),
+                                              (257, 64, 30, "rel"), (900, 40, None, "zero"), (150, 150, None, "abs"),
+                                              (200, 70, 0, "abs"), (4096, 100, 60, "rel")])
+def test_ptg_qrcp_persistent_equals_step_launches(monkeypatch, m, n, rank, tolmode):
+    """the persistent pivoted QR (one launch, a grid barrier per step, csrc/ptgen.hip qrcp_persist_kernel) against one
+    launch per step (PQD_PTG_QPERSIST=0): the same arithmetic, so Q, R, the pivots and the rank are equal bit for bit;
+    with one poll per barrier wait (PQD_PTG_QSPIN=1) the barrier times out, the factorization is rerun from the saved
+    copy (pqd_ptg_qr_counters counts it) and the results are still equal"""
+    import ctypes
+    from pyaceqd_amd import _lib, ptgen_gpu
+    monkeypatch.setenv("PQD_PTG_SMALL", "0")
+    rng = np.random.default_rng(m + 3 * n)
+    if rank == 0:
+        W = np.zeros((m, n), complex)
+    else:
+        W = _rand(rng, m, n, rank=rank, scale=None if rank else np.logspace(0, -14, n))
+    tol = {"abs": 1e-10 * np.max(np.linalg.norm(W, axis=0)), "rel": -1e-10, "zero": 0.0}[tolmode]
+    dW = _dev(W.T)                                 # the device (torch's HIP runtime) before the library's first call
+    out = {}
+    for mode in ("step", "persist", "timeout"):
+        monkeypatch.setenv("PQD_PTG_QPERSIST", "0" if mode == "step" else "1")
+        monkeypatch.setenv("PQD_PTG_QSPIN", "1" if mode == "timeout" else str(1 << 22))
+        fb0, fb1 = ctypes.c_int32(0), ctypes.c_int32(0)
+        _lib.check(_lib.lib().pqd_ptg_qr_counters(ctypes.byref(fb0)))
+        Qc, Rc, perm, k = ptgen_gpu.qr_cols(dW, pivot=True, tol=tol, unperm=tolmode == "rel")
+        _lib.check(_lib.lib().pqd_ptg_qr_counters(ctypes.byref(fb1)))
+        out[mode] = (Qc.cpu().numpy(), Rc.cpu().numpy(), perm.cpu().numpy(), k)
+        if mode == "timeout":
+            assert fb1.value > fb0.value          # n >= 40 workgroups: one poll cannot see them all arrive
+        else:
+            assert fb1.value == fb0.value
+    for mode in ("persist", "timeout"):
+        a, b = out["step"], out[mode]
+        assert a[3] == b[3] and np.array_equal(a[2], b[2])
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    Q, R, p, k = out["persist"][0].T, out["persist"][1].T, out["persist"][2], out["persist"][3]
+    if rank is not None:
+        assert k == rank
+    if k:
+        assert np.max(np.abs(Q.conj().T @ Q - np.eye(k))) < 1e-12
+        Wp = W if tolmode == "rel" else W[:, p]
+        assert np.linalg.norm(Wp - Q @ R) <= 1e-9 * max(np.linalg.norm(W), 1e-300)
+
+
 @pytest.mark.parametrize("small", ["1", "0"])
 @pytest.mark.parametrize("m,n,rank", [(80, 39, 13), (60, 40, None), (1205, 300, 120), (400, 250, None), (700, 11, 5),
                                       (150, 50, None)])
