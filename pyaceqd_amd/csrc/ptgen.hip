@@ -1396,7 +1396,8 @@ __global__ __launch_bounds__(256) void jac_block_kernel(JacArgs a, JacPersist q,
     if (blockIdx.x == 0 && tid == 0) *q.sweeps = sweep;
 }
 
-// persistent column-pivoted QR: every step in ONE launch, qr_step_wg_kernel's arithmetic. Workgroup g owns PHYSICAL
+// persistent Householder QR (column-pivoted, or plain: a.pivot == 0, no search, no stop, no norms): every step in ONE
+// launch, qr_step_wg_kernel's arithmetic. Workgroup g owns PHYSICAL
 // column g for the whole factorization and holds it in registers; the permutation lives in each workgroup's LDS (every
 // workgroup makes the same swap). Step k: the pivot search over the trailing norms (sc1 loads, the same scan and tie
 // rule as the launch path), the stop test, the swap; the pivot column's owner records the reflector, the trailing
@@ -1436,7 +1437,7 @@ __global__ __launch_bounds__(WG_T) void qrcp_persist_kernel(QRArgs a, QRPersist 
     for (; k < a.kmax; ++k) {
         const double* nin = a.norms + (size_t)(k & 1) * n;
         double* nout = a.norms + (size_t)((k + 1) & 1) * n;
-        if (tid < 64) {
+        if (a.pivot && tid < 64) {
             double best = -1.0;
             int bj = k;
             for (int jj = k + tid; jj < n; jj += 64) {
@@ -1454,15 +1455,17 @@ __global__ __launch_bounds__(WG_T) void qrcp_persist_kernel(QRArgs a, QRPersist 
             if (tid == 0) { s_p = bj; s_best = best; }
         }
         __syncthreads();
-        const int p = s_p;
-        const double sb = s_best;
-        if (a.rel2 > 0.0 && k == 0) {
-            lim = a.rel2 * sb;
-            if (g == 0 && tid == 0) *a.thr = lim;
-        }
-        if (sb <= lim) {
-            if (g == 0 && tid == 0) a.ctrl[0] = k;
-            break;
+        const int p = a.pivot ? s_p : k;  // plain QR: no search, no stop (s_perm stays the identity)
+        if (a.pivot) {
+            const double sb = s_best;
+            if (a.rel2 > 0.0 && k == 0) {
+                lim = a.rel2 * sb;
+                if (g == 0 && tid == 0) *a.thr = lim;
+            }
+            if (sb <= lim) {
+                if (g == 0 && tid == 0) a.ctrl[0] = k;
+                break;
+            }
         }
         const int cp = s_perm[p];  // the pivot's physical column
         __syncthreads();           // every thread has read s_perm[p] before the swap
@@ -1516,10 +1519,12 @@ __global__ __launch_bounds__(WG_T) void qrcp_persist_kernel(QRArgs a, QRPersist 
                         st16(rW, g * m + k, cj[e]);
                     }
                 }
-                wg_reduce<1>(r2, red[1]);
-                if (tid == 0)
-                    __hip_atomic_store((gu64*)(nout + g), (unsigned long long)__double_as_longlong(r2[0]),
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (a.pivot) {
+                    wg_reduce<1>(r2, red[1]);
+                    if (tid == 0)
+                        __hip_atomic_store((gu64*)(nout + g), (unsigned long long)__double_as_longlong(r2[0]),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
         }
         // ---- grid barrier
@@ -1779,18 +1784,19 @@ extern "C" int pqd_ptg_qr(void* stream, pqd_c128* Wp, int32_t m, int32_t n, int3
     const double rel2 = pivot && tol < 0.0 ? tol * tol : 0.0;
     void* base = nullptr;
     const bool small = small_ok() && (size_t)m * n <= (size_t)QS_MAX && n <= 256;
-    const bool pairs = !pivot && !small && kmax >= 2 && env_int("PQD_PTG_PAIR", 1) != 0;
     const int ept = env_int("PQD_PTG_WG", 1) ? wg_ept(m) : 0;
     // blocked factorization: PQD_PTG_BLOCKED=1 always, 0 never, default from 10^6 elements (the size where the
     // per-step trailing traffic of the column kernels starts to exceed the panels' extra launches; profiles/r04/ptgen)
     const int blk_env = env_int("PQD_PTG_BLOCKED", -1);
-    const bool blocked = !pivot && !small && m >= n && n > QB &&
+    // QRs whose columns fit in registers: every step in one persistent launch (PQD_PTG_QPERSIST=1: pivoted QRs, 2:
+    // pivoted and plain QRs; default 0: one launch per step). A plain QR then takes one reflector per step (no pairs)
+    const int qp_env = env_int("PQD_PTG_QPERSIST", 0);
+    const bool qpersist = !small && ept > 0 && kmax >= 2 && (pivot ? qp_env >= 1 : (qp_env >= 2 && blk_env != 1)) &&
+                          qrcp_persist_fits(ept, n);
+    const bool pairs = !pivot && !small && !qpersist && kmax >= 2 && env_int("PQD_PTG_PAIR", 1) != 0;
+    const bool blocked = !pivot && !small && !qpersist && m >= n && n > QB &&
                          (blk_env == 1 || (blk_env < 0 && (size_t)m * n >= (size_t)1000000));
     const bool qfb = !small && env_int("PQD_PTG_QFB", 1) != 0;
-    // column-pivoted QRs whose columns fit in registers: every step in one persistent launch (PQD_PTG_QPERSIST=1;
-    // default: one launch per step)
-    const bool qpersist = pivot && !small && ept > 0 && kmax >= 2 && env_int("PQD_PTG_QPERSIST", 0) != 0 &&
-                          qrcp_persist_fits(ept, n);
     const bool sepx = pairs || blocked;  // reflector columns in their own buffer X
     const size_t b_tau = al(kmax * sizeof(double2)), b_beta = al(kmax * sizeof(double)),
                  b_perm = al(2 * (size_t)n * sizeof(int)), b_norm = al(2 * (size_t)n * sizeof(double)),

@@ -1,6 +1,6 @@
 #!/bin/bash
 # (1) quad kernel without scratch vs the round-4 head (ab/libpqd_base.so): quad/branching/CW tests, C2 A/B x3;
-# (2) persistent pivoted QR: generator QR/SVD tests, then the biexciton generator with PQD_PTG_QPERSIST=1 / 0
+# (2) persistent QR: generator QR/SVD tests, then the biexciton generator with PQD_PTG_QPERSIST=0 / 1 (pivoted) / 2 (+plain)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 O=gpurun_out/qpersist; mkdir -p $O
 export TMPDIR=/tmp
@@ -15,7 +15,7 @@ done
 timeout -k 10 500 python -u -m pytest tests/test_gpu_ptgen.py -k "qr or svd" -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_ptgen.log 2>&1
 rc=$?; tail -2 $O/pytest_ptgen.log; case $rc in 0) ;; *) grep -E "^FAILED|Error|assert" $O/pytest_ptgen.log | head; echo "rc=$rc stop"; exit 1;; esac
 for r in 1 2; do
-  for P in 0 1; do
+  for P in 0 1 2; do
     PQD_PTG_QPERSIST=$P PQD_PTG_PHASES=1 timeout -k 10 200 python -u scripts/bench_ptgen.py --case bx05,bx01 --steps 25 > $O/ptg_$P.log 2>&1 || { tail -20 $O/ptg_$P.log; exit 1; }
     echo "round $r QPERSIST=$P: $(grep -E 'RESULT|PHASES' $O/ptg_$P.log | tr '\n' ' ')"
   done

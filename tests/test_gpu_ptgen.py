@@ -159,6 +159,38 @@ def test_ptg_qrcp_persistent_equals_step_launches(monkeypatch, m, n, rank, tolmo
         assert np.linalg.norm(Wp - Q @ R) <= 1e-9 * max(np.linalg.norm(W), 1e-300)
 
 
+@pytest.mark.parametrize("m,n", [(2048, 128), (1205, 300), (400, 250), (3000, 200), (257, 64), (4096, 100), (150, 150),
+                                 (100, 180)])
+def test_ptg_qr_persistent_plain_equals_step_launches(monkeypatch, m, n):
+    """plain Householder QR on the persistent kernel (PQD_PTG_QPERSIST=2) against one launch per reflector
+    (PQD_PTG_PAIR=0, PQD_PTG_BLOCKED=0): equal bit for bit, also after a forced barrier timeout; and against LAPACK's R"""
+    import ctypes
+    from pyaceqd_amd import _lib, ptgen_gpu
+    monkeypatch.setenv("PQD_PTG_SMALL", "0")
+    rng = np.random.default_rng(m + 5 * n)
+    W = _rand(rng, m, n, scale=np.logspace(0, -12, n))
+    dW = _dev(W.T)
+    out = {}
+    for mode in ("step", "persist", "timeout"):
+        monkeypatch.setenv("PQD_PTG_QPERSIST", "0" if mode == "step" else "2")
+        monkeypatch.setenv("PQD_PTG_PAIR", "0")
+        monkeypatch.setenv("PQD_PTG_BLOCKED", "0")
+        monkeypatch.setenv("PQD_PTG_QSPIN", "1" if mode == "timeout" else str(1 << 22))
+        fb0, fb1 = ctypes.c_int32(0), ctypes.c_int32(0)
+        _lib.check(_lib.lib().pqd_ptg_qr_counters(ctypes.byref(fb0)))
+        Qc, Rc, perm, k = ptgen_gpu.qr_cols(dW)
+        _lib.check(_lib.lib().pqd_ptg_qr_counters(ctypes.byref(fb1)))
+        out[mode] = (Qc.cpu().numpy(), Rc.cpu().numpy(), k)
+        assert (fb1.value > fb0.value) == (mode == "timeout")
+    for mode in ("persist", "timeout"):
+        assert out[mode][2] == out["step"][2] == min(m, n)
+        assert np.array_equal(out[mode][0], out["step"][0]) and np.array_equal(out[mode][1], out["step"][1])
+    Q, R = out["persist"][0].T, out["persist"][1].T
+    assert np.max(np.abs(Q.conj().T @ Q - np.eye(min(m, n)))) < 1e-13
+    Rn = np.linalg.qr(W, mode="r")
+    assert np.max(np.abs(R - Rn)) < 1e-12 * np.max(np.abs(Rn))
+
+
 @pytest.mark.parametrize("small", ["1", "0"])
 @pytest.mark.parametrize("m,n,rank", [(80, 39, 13), (60, 40, None), (1205, 300, 120), (400, 250, None), (700, 11, 5),
                                       (150, 50, None)])
