@@ -290,7 +290,8 @@ int pqd_ptg_jacobi(void* stream, pqd_c128* X, int32_t n, pqd_c128* V, double* si
 int pqd_ptg_counters(int32_t* jacobi_fallbacks);
 /* With PQD_PTG_QPERSIST=1, pqd_ptg_qr runs a column-pivoted QR whose columns fit in registers (m <= 4096) in one
  * persistent launch (workgroup g holds physical column g; a grid barrier per step) when its n workgroups can all be
- * resident; a timed-out barrier wait reruns it from a saved copy with one launch per step (the default path).
+ * resident; a timed-out barrier wait reruns it from a saved copy with one launch per step (the default path, which
+ * measured faster: profiles/r04/ptgen/qpersist/). PQD_PTG_QPERSIST=2 also takes plain QRs.
  * pqd_ptg_qr_counters: how many reruns happened in this process (diagnostics, tests). */
 int pqd_ptg_qr_counters(int32_t* qrcp_fallbacks);
 

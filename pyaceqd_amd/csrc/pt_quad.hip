@@ -60,15 +60,6 @@ __device__ __forceinline__ void quad_col(double2 a, bool mine, double2 (&R)[NCG]
 // 1000..1015, workgroup 0, wave 0 (a separate instantiation; the production kernel carries none of it)
 __device__ unsigned long long g_quad_stamps[16 * 16];
 
-// a per-lane value the compiler must treat as new at this point: addresses derived from it in the slow step are
-// computed there (a few VALU ops) instead of hoisted out of the step loop and kept live, in 64-bit pairs, across
-// the fast pairs that never use them (which spilled them to scratch)
-template <class T>
-__device__ __forceinline__ T opq(T v) {
-    asm volatile("" : "+v"(v));
-    return v;
-}
-
 // s_setprio takes an immediate
 __device__ __forceinline__ void set_prio(int k) {
     if (k <= 0) __builtin_amdgcn_s_setprio(0);
@@ -117,12 +108,11 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : (NCG =
     const int la = lane >> 4, lt = (lane >> 2) & 3, lc = lane & 3;
     const int traj = qvalid ? p.blk_traj[blk * 4 + lt] : -1;
     const int act = qvalid ? p.blk_act[blk * 4 + lt] : INT_MAX;
+    const int src = qvalid ? p.blk_src[blk * 4 + lt] : -1;
     const int wb = traj >= 0 ? p.wbeg[traj] : INT_MAX, we = traj >= 0 ? p.wend[traj] : -1;
     const int sys = traj >= 0 ? p.traj_sys[traj] : 0;
     int ev_cur = traj >= 0 ? p.ev_start[traj] : 0;
     const int ev_lim = traj >= 0 ? p.ev_start[traj + 1] : 0;
-    // the end of this slot's events, re-read where an event is consumed (slow steps) rather than kept live
-    auto ev_end = [&]() { const int t = opq(traj); return t >= 0 ? p.ev_start[t + 1] : 0; };
     const int2 wq = fw_win(p, sys);  // pulse window: M, F outside it are the system's idle operators (fw_M, fw_F)
     const int opi = lc * 4 + la;  // this lane's operator element Op[alpha' = lc][alpha = la]
     // ---- T-layout (l = 16 t + 4 k + alpha): the traces, four lanes per (trajectory, output k < 4), reduced over alpha
@@ -223,6 +213,7 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : (NCG =
         return f[fmul * opi];
     };
     auto ldS = [&](int n) { return p.sched[n < ns ? n : ns - 1]; };
+    const double2 ov = p.ovec[k2c * 4 + a2];  // T-layout: element (k2, a2) of the output rows (unfused steps)
     double2 fpre[2], wv[2];
     int sr[2];
     auto ldW = [&](int j, int n) {
@@ -262,11 +253,7 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : (NCG =
         const bool qlive = n <= q_hi;  // wave-uniform (per quad)
         // ------------------------------------------------ shared-trunk activations at the top of step n
         if (n == next_act) {
-            // the slot's source and column offset are re-read / re-derived here (activations are rare): kept live
-            // across the fast pairs they were spilled
-            const int ln = opq(lane), lt_ = (ln >> 2) & 3, la_ = ln >> 4, lc_ = ln & 3;
-            const int src = qvalid ? p.blk_src[blk * 4 + lt_] : -1;
-            const int sl = 16 * la_ + 4 * (src >= 0 ? src : 0) + lc_;
+            const int sl = 16 * la + 4 * (src >= 0 ? src : 0) + lc;
             double2 Rs[NCG];
 #pragma unroll
             for (int cg = 0; cg < NCG; ++cg) Rs[cg] = make_double2(__shfl(R[cg].x, sl), __shfl(R[cg].y, sl));
@@ -277,7 +264,7 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : (NCG =
                     for (int cg = 0; cg < NCG; ++cg) R[cg] = Rs[cg];
                     fz = fzs;
                 } else if (src <= -2) {
-                    const double2* ck = p.ck + (size_t)(-2 - src) * 4 * CHI + (size_t)la_ * CHI + CW * h + lc_;
+                    const double2* ck = p.ck + (size_t)(-2 - src) * 4 * CHI + (size_t)la * CHI + CW * h + lc;
 #pragma unroll
                     for (int cg = 0; cg < NCG; ++cg) R[cg] = ck[4 * cg];
                     fz = true;
@@ -320,14 +307,14 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : (NCG =
                     const bool mine = k0 < 9;
                     double2 a = c_zero();
                     if (k0 == 0) { a = fpre[S]; k0 = 9; }
-                    else if (k0 == 1) { a = fw_M(p, opq(sys), wq, 2 * n - 1, 16)[opq(opi)]; k0 = 2; }
+                    else if (k0 == 1) { a = fw_M(p, sys, wq, 2 * n - 1, 16)[opi]; k0 = 2; }
                     else if (k0 == 2) {
                         if (evn.x == n && evn.y == 1) {
-                            a = p.sop[(size_t)evn.z * 16 + opq(opi)];
+                            a = p.sop[(size_t)evn.z * 16 + opi];
                             ++ev_cur;
-                            evn = ev_cur < ev_end() ? p.ev[opq(ev_cur)] : make_int4(INT_MAX, 0, 0, 0);
+                            evn = ev_cur < ev_lim ? p.ev[ev_cur] : make_int4(INT_MAX, 0, 0, 0);
                         } else {
-                            a = fw_M(p, opq(sys), wq, 2 * n, 16)[opq(opi)];
+                            a = fw_M(p, sys, wq, 2 * n, 16)[opi];
                             k0 = 9;
                         }
                     }
@@ -349,17 +336,13 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : (NCG =
             for (int g = 1; g < NWG; ++g) r = c_add(r, rpp[g * 16 + 4 * t2 + a2]);
             const bool f2 = (fzb >> (4 * t2)) & 1;
             const bool win2 = traj2 >= 0 && n >= act2 && wb2 <= n && n <= we2;
-            // unfused: element (k2, a2) of the output rows, read here (slow steps) rather than held across the fast pairs
-            // (the loaded row passes opq so the select is not folded into a select of addresses, which would move the
-            // ring wv[] to scratch)
-            const double2 ou = p.ovec[opq(k2c * 4 + a2)];
-            const double2 x = quad_sum(c_mul(f2 ? wv[S] : make_double2(opq(ou.x), opq(ou.y)), r));
+            const double2 x = quad_sum(c_mul(f2 ? wv[S] : ov, r));
             if (a2 == 0 && win2 && k2 < NO) p.out[wo2 + (long long)(n - wb2) * NO + k2] = x;
             for (int kb = 4; kb < NO; kb += 4) {  // more than four outputs: further passes, rows loaded here
                 const int k = kb + k2 < NO ? kb + k2 : NO - 1;
                 const double2 w = f2 ? fw_W(p, sys2, wq2, n, 4)[k * 4 + a2] : p.ovec[k * 4 + a2];
                 const double2 y = quad_sum(c_mul(w, r));
-                if (a2 == 0 && win2 && kb + k2 < NO) p.out[opq(wo2 + (long long)(n - wb2) * NO + k2) + kb] = y;
+                if (a2 == 0 && win2 && kb + k2 < NO) p.out[wo2 + (long long)(n - wb2) * NO + kb + k2] = y;
             }
         }
         stamp(4);
@@ -420,12 +403,12 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : (NCG =
             while (__ballot(k0 < 9)) {
                 bool mine = k0 < 9;
                 double2 a = c_zero();
-                if (k0 == 0) { a = fw_M(p, opq(sys), wq, 2 * n + 1, 16)[opq(opi)]; k0 = 1; }
+                if (k0 == 0) { a = fw_M(p, sys, wq, 2 * n + 1, 16)[opi]; k0 = 1; }
                 else if (k0 == 1) {
                     if (evn.x == n + 1 && evn.y == 0) {
-                        a = p.sop[(size_t)evn.z * 16 + opq(opi)];
+                        a = p.sop[(size_t)evn.z * 16 + opi];
                         ++ev_cur;
-                        evn = ev_cur < ev_end() ? p.ev[opq(ev_cur)] : make_int4(INT_MAX, 0, 0, 0);
+                        evn = ev_cur < ev_lim ? p.ev[ev_cur] : make_int4(INT_MAX, 0, 0, 0);
                     } else {
                         mine = false;
                     }

@@ -1789,7 +1789,10 @@ extern "C" int pqd_ptg_qr(void* stream, pqd_c128* Wp, int32_t m, int32_t n, int3
     // per-step trailing traffic of the column kernels starts to exceed the panels' extra launches; profiles/r04/ptgen)
     const int blk_env = env_int("PQD_PTG_BLOCKED", -1);
     // QRs whose columns fit in registers: every step in one persistent launch (PQD_PTG_QPERSIST=1: pivoted QRs, 2:
-    // pivoted and plain QRs; default 0: one launch per step). A plain QR then takes one reflector per step (no pairs)
+    // pivoted and plain QRs; default 0: one launch per step). A plain QR then takes one reflector per step (no pairs).
+    // Measured slower than the launches (profiles/r04/ptgen/qpersist/: QRCP phases +8-13%, plain QRs +40%): each step
+    // is three dependent coherent round trips (the norm scan, the barrier, the pivot column), where back-to-back
+    // launches read the same data from L2
     const int qp_env = env_int("PQD_PTG_QPERSIST", 0);
     const bool qpersist = !small && ept > 0 && kmax >= 2 && (pivot ? qp_env >= 1 : (qp_env >= 2 && blk_env != 1)) &&
                           qrcp_persist_fits(ept, n);

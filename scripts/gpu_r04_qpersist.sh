@@ -4,6 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 O=gpurun_out/qpersist; mkdir -p $O
 export TMPDIR=/tmp
+if [ "${SKIP_QUAD:-0}" = 0 ]; then
 timeout -k 10 400 python -u -m pytest tests/test_gpu_quad.py tests/test_gpu_branching.py "tests/test_gpu_configs.py::test_cw_drive_matches_exact_lindblad_solution" -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_quad.log 2>&1
 rc=$?; tail -2 $O/pytest_quad.log; case $rc in 0) ;; *) grep -E "^FAILED|Error|assert" $O/pytest_quad.log | head; echo "rc=$rc stop"; exit 1;; esac
 for r in 1 2 3; do
@@ -12,6 +13,7 @@ for r in 1 2 3; do
     echo "round $r $L: $(grep -o '"pt_sweep_ms": [0-9.]*\|"frac_fp64": [0-9.]*' $O/q.log | tr '\n' ' ')"
   done
 done
+fi
 timeout -k 10 500 python -u -m pytest tests/test_gpu_ptgen.py -k "qr or svd" -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_ptgen.log 2>&1
 rc=$?; tail -2 $O/pytest_ptgen.log; case $rc in 0) ;; *) grep -E "^FAILED|Error|assert" $O/pytest_ptgen.log | head; echo "rc=$rc stop"; exit 1;; esac
 for r in 1 2; do

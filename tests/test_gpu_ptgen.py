@@ -142,9 +142,9 @@ def test_ptg_qrcp_persistent_equals_step_launches(monkeypatch, m, n, rank, tolmo
         Qc, Rc, perm, k = ptgen_gpu.qr_cols(dW, pivot=True, tol=tol, unperm=tolmode == "rel")
         _lib.check(_lib.lib().pqd_ptg_qr_counters(ctypes.byref(fb1)))
         out[mode] = (Qc.cpu().numpy(), Rc.cpu().numpy(), perm.cpu().numpy(), k)
-        if mode == "timeout":
+        if mode == "timeout" and rank != 0:       # (a zero matrix stops at step 0, before the first barrier)
             assert fb1.value > fb0.value          # n >= 40 workgroups: one poll cannot see them all arrive
-        else:
+        elif mode != "timeout":
             assert fb1.value == fb0.value
     for mode in ("persist", "timeout"):
         a, b = out["step"], out[mode]
