@@ -60,6 +60,16 @@ __device__ __forceinline__ void quad_col(double2 a, bool mine, double2 (&R)[NCG]
 // 1000..1015, workgroup 0, wave 0 (a separate instantiation; the production kernel carries none of it)
 __device__ unsigned long long g_quad_stamps[16 * 16];
 
+// a per-lane value the compiler must treat as new at this point: the slow step's operator and event addresses derived
+// from it are computed there (a few VALU ops) instead of hoisted out of the step loop and held, as 64-bit pairs,
+// across the fast pairs that never use them (C2 instance: 21 -> 8 spilled VGPRs, 64 -> 28 B scratch, sweep
+// 14.27 -> 14.21 ms; profiles/r04/quad/ab_v1.log)
+template <class T>
+__device__ __forceinline__ T opq(T v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
 // s_setprio takes an immediate
 __device__ __forceinline__ void set_prio(int k) {
     if (k <= 0) __builtin_amdgcn_s_setprio(0);
@@ -307,14 +317,14 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : (NCG =
                     const bool mine = k0 < 9;
                     double2 a = c_zero();
                     if (k0 == 0) { a = fpre[S]; k0 = 9; }
-                    else if (k0 == 1) { a = fw_M(p, sys, wq, 2 * n - 1, 16)[opi]; k0 = 2; }
+                    else if (k0 == 1) { a = fw_M(p, opq(sys), wq, 2 * n - 1, 16)[opq(opi)]; k0 = 2; }
                     else if (k0 == 2) {
                         if (evn.x == n && evn.y == 1) {
-                            a = p.sop[(size_t)evn.z * 16 + opi];
+                            a = p.sop[(size_t)evn.z * 16 + opq(opi)];
                             ++ev_cur;
-                            evn = ev_cur < ev_lim ? p.ev[ev_cur] : make_int4(INT_MAX, 0, 0, 0);
+                            evn = ev_cur < ev_lim ? p.ev[opq(ev_cur)] : make_int4(INT_MAX, 0, 0, 0);
                         } else {
-                            a = fw_M(p, sys, wq, 2 * n, 16)[opi];
+                            a = fw_M(p, opq(sys), wq, 2 * n, 16)[opq(opi)];
                             k0 = 9;
                         }
                     }
@@ -403,12 +413,12 @@ __global__ __launch_bounds__(64 * QPW * (CHI / (4 * NCG)), NCG == 2 ? 2 : (NCG =
             while (__ballot(k0 < 9)) {
                 bool mine = k0 < 9;
                 double2 a = c_zero();
-                if (k0 == 0) { a = fw_M(p, sys, wq, 2 * n + 1, 16)[opi]; k0 = 1; }
+                if (k0 == 0) { a = fw_M(p, opq(sys), wq, 2 * n + 1, 16)[opq(opi)]; k0 = 1; }
                 else if (k0 == 1) {
                     if (evn.x == n + 1 && evn.y == 0) {
-                        a = p.sop[(size_t)evn.z * 16 + opi];
+                        a = p.sop[(size_t)evn.z * 16 + opq(opi)];
                         ++ev_cur;
-                        evn = ev_cur < ev_lim ? p.ev[ev_cur] : make_int4(INT_MAX, 0, 0, 0);
+                        evn = ev_cur < ev_lim ? p.ev[opq(ev_cur)] : make_int4(INT_MAX, 0, 0, 0);
                     } else {
                         mine = false;
                     }
