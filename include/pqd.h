@@ -281,7 +281,9 @@ int pqd_ptg_qr(void* stream, pqd_c128* W, int32_t m, int32_t n, int32_t pivot, d
                pqd_c128* R, int32_t* perm, int32_t* rank);
 /* pqd_ptg_jacobi: one-sided Jacobi SVD of a square n x n X (overwritten): X V = U diag(sigma), columns rotated
  * until every pair satisfies |x_p^H x_q| <= tol |x_p| |x_q|; a column with |x_j| < zero_tol ||X||_F is treated as
- * zero (never rotated). Outputs: X <- U (unit columns, unsorted), V (n x n), sigma (n, unsorted), *sweeps (host). */
+ * zero (never rotated). Outputs: X <- U (unit columns, unsorted), V (n x n), sigma (n, unsorted), *sweeps (host):
+ * the sweeps run, the last one without a rotation, or max_sweeps + 1 when max_sweeps sweeps did not converge.
+ * Scratch is kept per (device, stream): calls on different streams or devices never share a buffer. */
 int pqd_ptg_jacobi(void* stream, pqd_c128* X, int32_t n, pqd_c128* V, double* sigma, double tol, double zero_tol,
                    int32_t max_sweeps, int32_t* sweeps);
 /* pqd_ptg_jacobi runs its sweeps in one persistent launch (a grid barrier per round) when n <= 1024; if a barrier

@@ -22,6 +22,7 @@
 // Layout: every matrix is column-major with leading dimension = rows (a row-major torch tensor of shape
 // (cols, rows) whose row j is column j). Complex numbers are double2 (pqd_c128).
 #include "pqd_common.h"
+#include <map>
 #include "../../include/pqd.h"
 
 #include <algorithm>
@@ -1070,6 +1071,7 @@ __global__ __launch_bounds__(QS_THREADS) void jac_small_kernel(double2* Xg, doub
         V[idx] = make_double2(i == j ? 1.0 : 0.0, 0.0);
     }
     int sweep = 0;
+    bool conv = false;
     for (; sweep < max_sweeps; ++sweep) {
         if (tid == 0) s_cnt = 0;
         __syncthreads();
@@ -1083,14 +1085,14 @@ __global__ __launch_bounds__(QS_THREADS) void jac_small_kernel(double2* Xg, doub
             }
             __syncthreads();
         }
-        if (s_cnt == 0) { ++sweep; break; }
+        if (s_cnt == 0) { ++sweep; conv = true; break; }
         __syncthreads();
     }
     for (int idx = tid; idx < n * n; idx += QS_THREADS) {
         Xg[idx] = X[idx];
         Vg[idx] = V[idx];
     }
-    if (tid == 0) *sweeps_out = sweep;
+    if (tid == 0) *sweeps_out = conv ? sweep : max_sweeps + 1;  // > max_sweeps: no convergence
 }
 
 // persistent one-sided Jacobi: every round of every sweep in ONE launch. Wave i of the grid owns tournament slot i;
@@ -1137,6 +1139,7 @@ __global__ __launch_bounds__(256) void jac_persist_kernel(JacArgs a, JacPersist 
     const __amdgpu_buffer_rsrc_t rV = __builtin_amdgcn_make_buffer_rsrc(a.V, 0, n * n * 16, 0x00020000);
     unsigned epoch = 0;
     int sweep = 0;
+    bool conv = false;
     if (tid == 0) s_abort = 0;
     for (; sweep < q.max_sweeps; ++sweep) {
         if (tid == 0) s_rot = 0;
@@ -1220,9 +1223,9 @@ __global__ __launch_bounds__(256) void jac_persist_kernel(JacArgs a, JacPersist 
         if (tid == 0)
             s_done = __hip_atomic_load((gu32*)(q.cnt + sweep), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
         __syncthreads();
-        if (s_done) { ++sweep; break; }
+        if (s_done) { ++sweep; conv = true; break; }
     }
-    if (blockIdx.x == 0 && tid == 0) *q.sweeps = sweep;
+    if (blockIdx.x == 0 && tid == 0) *q.sweeps = conv ? sweep : q.max_sweeps + 1;  // > max_sweeps: no convergence
 }
 
 // block one-sided Jacobi, persistent: columns dealt into blocks of JB = 4; workgroup i takes block pair i of a
@@ -1293,6 +1296,7 @@ __global__ __launch_bounds__(256) void jac_block_kernel(JacArgs a, JacPersist q,
     double2* sV = sm + 2 * JB * n;
     unsigned epoch = 0;
     int sweep = 0;
+    bool conv = false;
     if (tid == 0) s_abort = 0;
     for (; sweep < q.max_sweeps; ++sweep) {
         if (tid == 0) s_rot = 0;
@@ -1391,9 +1395,9 @@ __global__ __launch_bounds__(256) void jac_block_kernel(JacArgs a, JacPersist q,
         if (tid == 0)
             s_done = __hip_atomic_load((gu32*)(q.cnt + sweep), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
         __syncthreads();
-        if (s_done) { ++sweep; break; }
+        if (s_done) { ++sweep; conv = true; break; }
     }
-    if (blockIdx.x == 0 && tid == 0) *q.sweeps = sweep;
+    if (blockIdx.x == 0 && tid == 0) *q.sweeps = conv ? sweep : q.max_sweeps + 1;  // > max_sweeps: no convergence
 }
 
 // persistent Householder QR (column-pivoted, or plain: a.pivot == 0, no search, no stop, no norms): every step in ONE
@@ -1590,33 +1594,46 @@ int perr(int code, const char* msg) {
 std::atomic<int> g_jac_fallbacks{0};  // persistent Jacobi launches rerun per round (barrier timeout)
 std::atomic<int> g_qr_fallbacks{0};   // persistent QRCP launches rerun one launch per step (barrier timeout)
 
-// per-process scratch (the generator runs one factorization at a time per stream; guarded for safety)
+// scratch per (device, stream): a factorization's kernels stay queued after the call returns (pqd_ptg_qr without
+// pivoting does not synchronise), so a call on another stream or device must not reuse the same buffer.
+// Calls are serialised by g_mu; the buffer of a stream grows (after synchronising that stream) and is kept.
 std::mutex g_mu;
 struct Scratch {
     void* p = nullptr;
     size_t bytes = 0;
-} g_scr;
-hipError_t scratch(size_t bytes, void** out) {
-    if (bytes > g_scr.bytes) {
-        if (g_scr.p) {
-            hipError_t e = hipDeviceSynchronize();
+};
+std::map<std::pair<int, hipStream_t>, Scratch> g_scr;
+hipError_t scratch(hipStream_t s, size_t bytes, void** out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    Scratch& sc = g_scr[std::make_pair(dev, s)];
+    if (bytes > sc.bytes) {
+        if (sc.p) {
+            e = hipStreamSynchronize(s);
             if (e != hipSuccess) return e;
-            e = hipFree(g_scr.p);
+            e = hipFree(sc.p);
             if (e != hipSuccess) return e;
-            g_scr.p = nullptr;
+            sc.p = nullptr;
         }
-        hipError_t e = hipMalloc(&g_scr.p, bytes);
-        if (e != hipSuccess) { g_scr.bytes = 0; return e; }
-        g_scr.bytes = bytes;
+        e = hipMalloc(&sc.p, bytes);
+        if (e != hipSuccess) { sc.bytes = 0; return e; }
+        sc.bytes = bytes;
     }
-    *out = g_scr.p;
+    *out = sc.p;
     return hipSuccess;
+}
+// the current device (function attributes and occupancy answers are per device)
+int cur_dev() {
+    int d = 0;
+    return hipGetDevice(&d) == hipSuccess && d >= 0 && d < 64 ? d : 0;
 }
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
-bool g_attr_done = false;
+unsigned long long g_attr_done = 0;  // bit d: the attributes are set on device d
 hipError_t small_attrs() {
-    if (g_attr_done) return hipSuccess;
+    const int dev = cur_dev();
+    if (g_attr_done >> dev & 1ull) return hipSuccess;
     const int lds = QS_MAX * (int)sizeof(double2);
     hipError_t e = hipSuccess;
     for (const void* f : {(const void*)qr_small_kernel<0>, (const void*)qr_small_kernel<1>,
@@ -1627,7 +1644,7 @@ hipError_t small_attrs() {
     }
     e = hipFuncSetAttribute((const void*)jac_small_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
-    g_attr_done = true;
+    g_attr_done |= 1ull << dev;
     return hipSuccess;
 }
 
@@ -1677,12 +1694,13 @@ const void* qrcp_persist_fn(int ept) {
     }
 }
 bool qrcp_persist_fits(int ept, int n) {
-    static int cus = 0;
-    static int per_cu[17] = {0};
+    static int cus_d[64] = {0};
+    static int per_cu_d[64][17] = {{0}};
+    const int dev = cur_dev();
+    int& cus = cus_d[dev];
+    int* per_cu = per_cu_d[dev];
     if (!cus) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             return false;
     }
     if (!per_cu[ept]) {
@@ -1806,7 +1824,7 @@ extern "C" int pqd_ptg_qr(void* stream, pqd_c128* Wp, int32_t m, int32_t n, int3
                  b_ctrl = al(64 * sizeof(int)), b_x = sepx ? al((size_t)m * kmax * sizeof(double2)) : 0,
                  b_blk = (blocked || qfb) ? block_bytes(m, n) : 0,
                  b_bak = qpersist ? al((size_t)m * n * sizeof(double2)) : 0;
-    PCHK(scratch(2 * b_tau + b_beta + b_perm + b_norm + b_ctrl + b_x + b_blk + b_bak, &base));
+    PCHK(scratch(s, 2 * b_tau + b_beta + b_perm + b_norm + b_ctrl + b_x + b_blk + b_bak, &base));
     char* c = static_cast<char*>(base);
     QRArgs a;
     a.W = W; a.m = m; a.n = n; a.kmax = kmax; a.pivot = pivot ? 1 : 0; a.tol2 = tol2; a.rel2 = rel2;
@@ -1949,7 +1967,7 @@ extern "C" int pqd_ptg_jacobi(void* stream, pqd_c128* Xp, int32_t n, pqd_c128* V
     // counters, then a copy of X: a persistent launch whose grid barrier times out (workgroups not co-resident, e.g.
     // under contention from other work on the device) is rerun from this copy with one launch per round
     const size_t b_cnt = al((64 + 200) * sizeof(int));
-    PCHK(scratch(b_cnt + al((size_t)n * n * sizeof(double2)), &base));
+    PCHK(scratch(s, b_cnt + al((size_t)n * n * sizeof(double2)), &base));
     int* cnt = static_cast<int*>(base);
     double2* Xbak = reinterpret_cast<double2*>(static_cast<char*>(base) + b_cnt);
     double* zero2 = reinterpret_cast<double*>(cnt + 8);
@@ -1990,12 +2008,13 @@ extern "C" int pqd_ptg_jacobi(void* stream, pqd_c128* Xp, int32_t n, pqd_c128* V
             const bool jblock = env_int("PQD_PTG_JBLOCK", 1) != 0 && epl <= 8 && lds_blk <= (size_t)JB_LDS_MAX &&
                                 nblk >= 2;
             if (jblock) {
-                static bool attr = false;
-                if (!attr) {
+                static unsigned long long attr = 0;  // bit d: set on device d
+                const int dev = cur_dev();
+                if (!(attr >> dev & 1ull)) {
                     for (const void* f : {(const void*)jac_block_kernel<1>, (const void*)jac_block_kernel<2>,
                                           (const void*)jac_block_kernel<4>, (const void*)jac_block_kernel<8>})
                         PCHK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, JB_LDS_MAX));
-                    attr = true;
+                    attr |= 1ull << dev;
                 }
                 const dim3 gb(nblk / 2);
                 switch (epl) {
@@ -2026,6 +2045,7 @@ extern "C" int pqd_ptg_jacobi(void* stream, pqd_c128* Xp, int32_t n, pqd_c128* V
             }
         }
         if (!persist) {
+            bool conv = false;
             for (; sweeps < max_sweeps;) {
                 PCHK(hipMemsetAsync(cnt, 0, sizeof(int), s));
                 for (int t = 0; t < a.nn - 1; ++t)
@@ -2035,8 +2055,9 @@ extern "C" int pqd_ptg_jacobi(void* stream, pqd_c128* Xp, int32_t n, pqd_c128* V
                 PCHK(hipMemcpyAsync(&h, cnt, sizeof(int), hipMemcpyDeviceToHost, s));
                 PCHK(hipStreamSynchronize(s));
                 ++sweeps;
-                if (h == 0) break;
+                if (h == 0) { conv = true; break; }
             }
+            if (!conv) sweeps = max_sweeps + 1;
         }
     }
     hipLaunchKernelGGL(jac_finish_kernel, dim3((n + 3) / 4), dim3(256), 0, s, X, n, sigma);

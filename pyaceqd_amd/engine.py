@@ -97,6 +97,7 @@ class ProcessTensor:
     gmap: np.ndarray
     n_init: int = None
     dt: Optional[float] = None
+    meta: Optional[dict] = None   # generation parameters (ptgen.generation_key); stored by pt.save_pt
 
     def __post_init__(self):
         self.Q = _c(self.Q)
@@ -227,6 +228,10 @@ def _prep(system, grid, rho0, out_ops, traj, pt, ctx):
     if pt is not None:
         if pt.gmap.shape[0] != N * N:
             raise ValueError(f"PT gmap has {pt.gmap.shape[0]} entries, system needs {N * N}")
+        if pt.dt is not None and abs(float(pt.dt) - float(grid.dt)) > 1e-9 * abs(float(grid.dt)):
+            # a PT is a discretisation at its own dt (the eta_k are integrals over dt-wide slices): propagating it
+            # on another grid is wrong physics, not a numerical detail
+            raise ValueError(f"PT was generated for dt = {pt.dt}, the grid has dt = {grid.dt}")
         pth = pt.handle(ctx, N)
         sched = pt.schedule(max(1, grid.n_steps))
     tsys = np.ascontiguousarray(np.zeros(max(1, traj.n_traj)) if traj.system is None else traj.system, dtype=np.int32)

@@ -13,6 +13,8 @@ absent, so round 1 ships:
     known-answer test against the equivalent Lindblad dissipator.
 The Gaussian-bath PT generator itself (QDPhonon J(omega), SVD compression) is SURVEY.md §8f rank 1.
 """
+import json
+
 import numpy as np
 
 from .engine import ProcessTensor
@@ -43,9 +45,12 @@ def schedule_info(n_init, n_slices):
 
 
 def save_pt(path, pt: ProcessTensor, dim=None):
+    """pqd-pt-v1 container. `meta` (the generation parameters, ptgen.generation_key) is stored as JSON text so a cached
+    PT can be checked against the parameters of a later call (general_system._resolve_pt)."""
+    meta = "" if pt.meta is None else json.dumps(pt.meta, sort_keys=True)
     np.savez(path, format="pqd-pt-v1", Q=pt.Q, closure=pt.closure, closure0=pt.closure0, bond0=pt.bond0,
              gmap=pt.gmap, n_init=pt.n_init, dt=np.nan if pt.dt is None else pt.dt,
-             dim=-1 if dim is None else dim)
+             dim=-1 if dim is None else dim, meta=meta)
 
 
 def load_pt(path) -> ProcessTensor:
@@ -53,8 +58,10 @@ def load_pt(path) -> ProcessTensor:
     if str(z["format"]) != "pqd-pt-v1":
         raise ValueError(f"{path}: not a pqd-pt-v1 file")
     dt = float(z["dt"])
+    meta = str(z["meta"]) if "meta" in z.files else ""
     return ProcessTensor(Q=z["Q"], closure=z["closure"], closure0=z["closure0"], bond0=z["bond0"], gmap=z["gmap"],
-                         n_init=int(z["n_init"]), dt=None if np.isnan(dt) else dt)
+                         n_init=int(z["n_init"]), dt=None if np.isnan(dt) else dt,
+                         meta=json.loads(meta) if meta else None)
 
 
 def synthetic_pt(boson_op, chi, n_init=1, n_rep=1, seed=1234, eps=0.05, structured=True, dictionary=False,

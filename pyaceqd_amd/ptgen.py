@@ -346,21 +346,93 @@ def build_gaussian_pt(boson_op, dt, eta, delta_pol=0.0, n_init=None, threshold=1
                          n_init=n_init if repeat else S - 1, dt=dt)
 
 
-def qd_phonon_pt(boson_op, dt, t_mem=20.48, ae=3.0, temperature=1.0, threshold=1e-10, factor_ah=None,
-                 boson_e_max=7.0, J_file=None, use_infinite=False, max_bond=None, n_init=None, verbose=False):
-    """The PT of general_system.py:152-211's generate file, from its own parameters. The bond is capped at what
-    the sweep kernel holds in LDS: 128 for N <= 4, 64 above."""
-    if max_bond is None:
-        max_bond = 128 if np.asarray(boson_op).shape[0] <= 4 else 64
+def infinite_memory_steps(eta, boson_op, threshold):
+    """Memory K (in steps) of the `use_Gaussian_infinite` PT (general_system.py:150-151, 165-167: no `t_mem` line, the
+    generate file keeps `te 2*t_mem` and `threshold`). ACE's infinite-memory construction is not visible offline; here
+    the memory is the bath's own: the shortest K whose neglected couplings cannot move an influence value by more than
+    the compression threshold per step,
+        max|xi| max|lambda| sum_{k = K+1 .. k_cap} |eta_k| <= threshold,
+    with eta computed to k_cap = len(eta) - 1 = round(2 t_mem / dt), the `te` horizon the generate file still writes
+    (ACE propagates the generation to te, so no correlation longer than te can enter its PT either). Returns
+    (K, converged): converged is False when the tail never drops below the threshold inside te (K = k_cap then;
+    e.g. a_e = 3 nm, whose eta_k keep a ~1e-9 floor from the hard Boson_E_max cut of J)."""
+    lam = np.real(np.diag(np.asarray(boson_op)))
+    s = float(np.max(np.abs(lam))) * float(np.max(np.abs(lam[:, None] - lam[None, :])))
+    a = np.abs(np.asarray(eta)[1:])
+    k_cap = len(a)
+    if k_cap == 0 or s == 0.0:
+        return max(k_cap, 0), True
+    tail = np.concatenate([np.cumsum(a[::-1])[::-1], [0.0]])       # tail[K] = sum_{k > K} |eta_k|, K = 0..k_cap
+    K = int(np.nonzero(s * tail <= threshold)[0][0])              # tail[k_cap] = 0: always found
+    return max(1, K), K < k_cap
+
+
+def qd_phonon_eta(boson_op, dt, t_mem=20.48, ae=3.0, temperature=1.0, threshold=1e-10, factor_ah=None,
+                  boson_e_max=7.0, J_file=None, use_infinite=False, K=None):
+    """(eta[0..K], polaron shift, info) of the generate file's bath: J from QDPhonon(a_e, a_h) or `Boson_J_from_file`,
+    memory K = round(t_mem / dt) (`t_mem`, use_Gaussian_repeat) or infinite_memory_steps (use_Gaussian_infinite).
+    K (int) overrides the memory (the memory-convergence tests)."""
     if J_file is not None:
         J = J_from_file(J_file)
     else:
         ah = None if factor_ah is None else ae / factor_ah
         J = lambda w: qd_phonon_J(w, ae=ae, ah=ah)  # noqa: E731
-    n_mem = max(1, int(round(t_mem / dt)))
+    info = {"infinite": bool(use_infinite)}
+    if K is not None:
+        n_mem = int(K)
+    elif use_infinite:
+        k_cap = max(1, int(round(2 * t_mem / dt)))
+        eta, _ = eta_coefficients(J, temperature, dt, k_cap, e_max=boson_e_max)
+        n_mem, conv = infinite_memory_steps(eta, boson_op, threshold)
+        info.update(k_cap=k_cap, converged=bool(conv))
+    else:
+        n_mem = max(1, int(round(t_mem / dt)))
     eta, delta = eta_coefficients(J, temperature, dt, n_mem, e_max=boson_e_max)
-    return build_gaussian_pt(boson_op, dt, eta, delta, n_init=n_init, threshold=threshold, max_bond=max_bond,
-                             repeat=True, verbose=verbose)
+    info["K"] = int(n_mem)
+    return eta, delta, info
+
+
+def generation_key(boson_op, dt, t_mem, ae, temperature, threshold, factor_ah, boson_e_max, J_file, use_infinite,
+                   max_bond):
+    """The parameters that decide a generated PT (stored in its .npz as `meta`, compared when a cache is reused):
+    coupling eigenvalues, dt, bath (a_e, a_h factor or the J file's content hash), temperature, threshold, E_max,
+    memory mode (t_mem, or infinite: then t_mem only bounds the horizon te = 2 t_mem) and the bond cap."""
+    import hashlib
+    lam = [float(x) for x in np.round(np.real(np.diag(np.asarray(boson_op))), 12)]
+    key = {"lam": lam, "dt": float(dt), "temperature": float(temperature), "threshold": float(threshold),
+           "boson_e_max": float(boson_e_max), "infinite": bool(use_infinite), "t_mem": float(t_mem),
+           "max_bond": int(max_bond)}
+    if J_file is not None:
+        with open(J_file, "rb") as f:
+            key["J_sha1"] = hashlib.sha1(f.read()).hexdigest()
+    else:
+        key["ae"] = float(ae)
+        key["factor_ah"] = None if factor_ah is None else float(factor_ah)
+    return key
+
+
+def default_max_bond(boson_op):
+    """the sweep kernel's LDS-resident bond: 128 for N <= 4, 64 above"""
+    return 128 if np.asarray(boson_op).shape[0] <= 4 else 64
+
+
+def qd_phonon_pt(boson_op, dt, t_mem=20.48, ae=3.0, temperature=1.0, threshold=1e-10, factor_ah=None,
+                 boson_e_max=7.0, J_file=None, use_infinite=False, max_bond=None, n_init=None, verbose=False, K=None):
+    """The PT of general_system.py:152-211's generate file, from its own parameters: memory t_mem (repeat) or the
+    bath's own memory (use_infinite, infinite_memory_steps). The bond is capped at what the sweep kernel holds in
+    LDS: 128 for N <= 4, 64 above. The result carries its generation parameters in `meta`."""
+    if max_bond is None:
+        max_bond = default_max_bond(boson_op)
+    eta, delta, info = qd_phonon_eta(boson_op, dt, t_mem, ae, temperature, threshold, factor_ah, boson_e_max, J_file,
+                                     use_infinite, K)
+    if verbose and use_infinite:
+        print("ptgen: infinite memory K = {} steps ({})".format(
+            info["K"], "converged" if info.get("converged", True) else "capped at te = 2 t_mem"))
+    pt = build_gaussian_pt(boson_op, dt, eta, delta, n_init=n_init, threshold=threshold, max_bond=max_bond,
+                           repeat=True, verbose=verbose)
+    pt.meta = dict(generation_key(boson_op, dt, t_mem, ae, temperature, threshold, factor_ah, boson_e_max, J_file,
+                                  use_infinite, max_bond), generator="host", tail="svd", **info)
+    return pt
 
 
 def pt_cache_name(system_prefix, ae, temperature, threshold, t_mem, dt, J_file=None, use_infinite=False):

@@ -33,6 +33,7 @@ _DEBUG = bool(int(os.environ.get("PQD_PTG_DEBUG", "0") or 0))
 # PQD_PTG_PHASES=1: wall time per compression phase (synchronising: diagnostics only, scripts/bench_ptgen.py)
 _PHASES = {"rcanon": 0.0, "svd": 0.0, "lr": 0.0} if os.environ.get("PQD_PTG_PHASES") == "1" else None
 _STATS = []  # (kind, sizes...) per factorization when PQD_PTG_DEBUG=1 (scripts/bench_ptgen.py --stats)
+LAST_SWEEPS = 0  # sweeps of the last jacobi_cols call (tests)
 RETRIES = []  # (n, attempt) of every boundary SVD whose Jacobi needed another attempt (svd below)
 
 
@@ -43,8 +44,9 @@ def _torch():
     return torch
 
 
-def _stream(torch):
-    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+def _stream(torch, dev=None):
+    """the current stream of the tensor's device (the library keys its scratch by device and stream)"""
+    return C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
 
 def qr_cols(Wc, pivot=False, tol=0.0, unperm=False):
@@ -61,10 +63,11 @@ def qr_cols(Wc, pivot=False, tol=0.0, unperm=False):
     R = torch.empty(max(kmax, 1) * n, dtype=torch.complex128, device=W.device)
     perm = torch.empty(n, dtype=torch.int32, device=W.device)
     rank = C.c_int32(0)
-    _lib.check(_lib.lib().pqd_ptg_qr(_stream(torch), C.c_void_p(W.data_ptr()), int(m), int(n),
-                                     (2 if unperm else 1) if pivot else 0,
-                                     float(tol), C.c_void_p(Q.data_ptr()), C.c_void_p(R.data_ptr()),
-                                     C.c_void_p(perm.data_ptr()), C.byref(rank)))
+    with torch.cuda.device(W.device):   # the launches go to W's device, on that device's current stream
+        _lib.check(_lib.lib().pqd_ptg_qr(_stream(torch, W.device), C.c_void_p(W.data_ptr()), int(m), int(n),
+                                         (2 if unperm else 1) if pivot else 0,
+                                         float(tol), C.c_void_p(Q.data_ptr()), C.c_void_p(R.data_ptr()),
+                                         C.c_void_p(perm.data_ptr()), C.byref(rank)))
     k = rank.value
     if _DEBUG:
         _STATS.append(("qrcp" if pivot else "qr", m, n, k))
@@ -89,10 +92,13 @@ def jacobi_cols(Xc, tol=None, max_sweeps=60, zero_tol=1e-16):
     V = torch.empty((n, n), dtype=torch.complex128, device=X.device)
     sig = torch.empty(n, dtype=torch.float64, device=X.device)
     sw = C.c_int32(0)
-    _lib.check(_lib.lib().pqd_ptg_jacobi(_stream(torch), C.c_void_p(X.data_ptr()), int(n), C.c_void_p(V.data_ptr()),
-                                         C.c_void_p(sig.data_ptr()), float(tol), float(zero_tol), int(max_sweeps),
-                                         C.byref(sw)))
-    if sw.value >= max_sweeps:
+    with torch.cuda.device(X.device):
+        _lib.check(_lib.lib().pqd_ptg_jacobi(_stream(torch, X.device), C.c_void_p(X.data_ptr()), int(n),
+                                             C.c_void_p(V.data_ptr()), C.c_void_p(sig.data_ptr()), float(tol),
+                                             float(zero_tol), int(max_sweeps), C.byref(sw)))
+    global LAST_SWEEPS
+    LAST_SWEEPS = sw.value
+    if sw.value > max_sweeps:   # the library reports max_sweeps + 1 when the last allowed sweep still rotated
         raise _lib.PQDError(f"pqd_ptg_jacobi: no convergence in {max_sweeps} sweeps (n = {n})")
     if _DEBUG:
         _STATS.append(("jacobi", n, sw.value))
@@ -385,16 +391,18 @@ def build_gaussian_pt_gpu(boson_op, dt, eta, delta_pol=0.0, n_init=None, thresho
 
 def qd_phonon_pt_gpu(boson_op, dt, t_mem=20.48, ae=3.0, temperature=1.0, threshold=1e-10, factor_ah=None,
                      boson_e_max=7.0, J_file=None, use_infinite=False, max_bond=None, n_init=None, verbose=False,
-                     tail="qrcp"):
-    """ptgen.qd_phonon_pt on the GPU: the PT of general_system.py:152-211's generate file, from its parameters."""
+                     tail="qrcp", K=None):
+    """ptgen.qd_phonon_pt on the GPU: the PT of general_system.py:152-211's generate file, from its parameters (memory
+    t_mem, or the bath's own memory with use_infinite: ptgen.infinite_memory_steps). Carries `meta`."""
     if max_bond is None:
-        max_bond = 128 if np.asarray(boson_op).shape[0] <= 4 else 64
-    if J_file is not None:
-        J = ptgen.J_from_file(J_file)
-    else:
-        ah = None if factor_ah is None else ae / factor_ah
-        J = lambda w: ptgen.qd_phonon_J(w, ae=ae, ah=ah)  # noqa: E731
-    n_mem = max(1, int(round(t_mem / dt)))
-    eta, delta = ptgen.eta_coefficients(J, temperature, dt, n_mem, e_max=boson_e_max)
-    return build_gaussian_pt_gpu(boson_op, dt, eta, delta, n_init=n_init, threshold=threshold, max_bond=max_bond,
-                                 repeat=True, verbose=verbose, tail=tail)
+        max_bond = ptgen.default_max_bond(boson_op)
+    eta, delta, info = ptgen.qd_phonon_eta(boson_op, dt, t_mem, ae, temperature, threshold, factor_ah, boson_e_max,
+                                           J_file, use_infinite, K)
+    if verbose and use_infinite:
+        print("ptgen_gpu: infinite memory K = {} steps ({})".format(
+            info["K"], "converged" if info.get("converged", True) else "capped at te = 2 t_mem"), flush=True)
+    pt = build_gaussian_pt_gpu(boson_op, dt, eta, delta, n_init=n_init, threshold=threshold, max_bond=max_bond,
+                               repeat=True, verbose=verbose, tail=tail)
+    pt.meta = dict(ptgen.generation_key(boson_op, dt, t_mem, ae, temperature, threshold, factor_ah, boson_e_max,
+                                        J_file, use_infinite, max_bond), generator="gpu", tail=tail, **info)
+    return pt

@@ -329,6 +329,7 @@ def tl_threeoptwotime_phonons_dm(system, t_axis, *pulses, t_mem=10, opA="|1><0|_
     ABC = A @ B @ Cm
     Bt = B.T.reshape(dim * dim)
     r0 = np.asarray(rho0, dtype=complex).copy().reshape(dim ** 2)
+    tails = _Tails()
     for i in range(len(t_mem_indices)):
         dm = dms_tauc[i]
         n_steps = 0 if i == 0 else int(np.round(t_axis[i] / dt, 6))
@@ -339,7 +340,7 @@ def tl_threeoptwotime_phonons_dm(system, t_axis, *pulses, t_mem=10, opA="|1><0|_
         for j in range(n_map):
             rho_t_mto = dm[j + n_steps] @ r0
             G[i, j + 1] = Bt @ rho_t_mto
-        _tail_rows(G, i, rho_t_mto, tl_map2, n_map, n_tau - n_map, Bt)
+        tails.add(i, rho_t_mto, n_map, n_tau - n_map)
     tl_1, tl_2 = dms_separated[0], dms_separated[1]
     for i in range(len(t_mem_indices), len(t_axis)):
         rho_t = r0.copy()
@@ -352,14 +353,29 @@ def tl_threeoptwotime_phonons_dm(system, t_axis, *pulses, t_mem=10, opA="|1><0|_
         for j in range(tl_2.shape[0]):
             rho_t = tl_2[j] @ rho_t
             G[i, j + 1] = Bt @ rho_t
-        _tail_rows(G, i, rho_t, tl_map2, tl_2.shape[0], n_tau - tl_2.shape[0], Bt)
+        tails.add(i, rho_t, tl_2.shape[0], n_tau - tl_2.shape[0])
+    tails.run(G, tl_map2, Bt)
     return t_axis, tau, G
 
 
-def _tail_rows(G, i, x, tl_map2, col0, n, Bt):
-    """G[i, col0 + 1 + j] = Bt . tl_map2^{j+1} x on the GPU (pqd_map_tail)"""
-    if n > 0:
-        G[i, col0 + 1: col0 + 1 + n] = propagate_tau_module.map_tail(tl_map2, np.asarray(x)[:, None], Bt, n)[0]
+class _Tails:
+    """The tau tails G[i, col0 + 1 + j] = Bt . tl_map2^{j+1} x_i of many rows, gathered by (col0, length) and run as
+    one pqd_map_tail call per group on the GPU (one call per row paid its allocations, launch and sync
+    once per t1 row)."""
+
+    def __init__(self):
+        self.groups = {}
+
+    def add(self, i, x, col0, n):
+        if n > 0:
+            self.groups.setdefault((int(col0), int(n)), []).append((i, np.array(x, dtype=complex)))
+
+    def run(self, G, tl_map2, Bt):
+        for (col0, n), rows in self.groups.items():
+            X = np.stack([x for _, x in rows], axis=1)
+            out = propagate_tau_module.map_tail(tl_map2, X, Bt, n)
+            for k, (i, _) in enumerate(rows):
+                G[i, col0 + 1: col0 + 1 + n] = out[k]
 
 
 def _tl_stationary_three_op(system, t_axis, pulses, t_mem, ops, tau_max, dt, rho0, options, mtos_dyn):

@@ -403,3 +403,92 @@ def test_gpu_generator_biexciton_reference_default_timed():
     # its truncation error (the bond cap of 128 binds here; measured 1.2e-7 after 120 steps)
     inf = influence(pt, [np.zeros(n, dtype=int) for n in (1, 10, 82, 120)])
     assert np.max(np.abs(inf - 1)) < 1e-6
+
+
+# ---------------------------------------------------- use_infinite at the tls defaults
+def test_tls_reference_default_phonons_ibm_on_hip(tmp_path):
+    """tls(phonons=True) at the reference's own defaults (tls.py:16-18: dt 0.1, a_e 5 nm, 4 K, threshold 8,
+    use_infinite=True) through the drop-in driver: the PT generated on the GPU with the bath's own memory (K = 65 of
+    the te = 12.8 ps horizon, converged), propagated on the HIP sweep, an undriven dot from (|0> + |1>)/sqrt 2
+    against the closed-form independent-boson coherence (continuous integral, independent quadrature) for 40 ps.
+    The bound is the generator's own accuracy at threshold 1e-8 (measured 6.1e-4 relative after 400 steps with the
+    host generator; 3.2e-5 at threshold 1e-10: the bond truncation, not the memory, sets it)."""
+    from pyaceqd_amd.two_level_system.tls import tls
+    t_end = 40.0
+    res = tls(0, t_end, phonons=True, rho0=0.5 * np.ones((2, 2), complex), output_ops=["|0><1|_2", "|0><0|_2"],
+              temp_dir=str(tmp_path) + os.sep)
+    from pyaceqd_amd.pt import load_pt
+    f = [x for x in os.listdir(tmp_path) if x.endswith(".pt.npz")]
+    assert len(f) == 1
+    meta = load_pt(str(tmp_path / f[0])).meta
+    assert meta["infinite"] and meta["converged"] and meta["K"] == 65 and meta["generator"] == "gpu"
+    J = lambda w: ptgen.qd_phonon_J(w, ae=5.0)  # noqa: E731
+    t = np.real(res[0])
+    ex = ptgen_oracle.ibm_coherence_exact(J, 4.0, t)
+    err = np.abs(res[1] - ex) / np.abs(ex)
+    print(f"tls default phonons: max rel err {err.max():.2e} (at {t[np.argmax(err)]:.1f} ps), K {meta['K']}")
+    assert np.max(err) < 1.5e-3
+    assert np.max(np.abs(res[2] - 0.5)) < 1e-9          # populations do not move in the IBM
+
+
+def test_gpu_infinite_memory_pt_converged_at_tls_default():
+    """the GPU-generated use_infinite PT at the tls defaults (K = 65, threshold 1e-8) against the same generator at
+    twice the memory (K = 130): influence values of 200 random paths over the explicit slices (<= 140 steps) agree to
+    <= 10 x threshold; over 400-step paths (repeated slice included) the doubled memory moves them by no more than
+    twice what another compression of the same memory does (the SVD tail instead of the QRCP tail): the memory is
+    converged to below the compression's own accumulated truncation (~threshold per step)"""
+    from pyaceqd_amd import ptgen_gpu
+    B = np.diag([0.0, 1.0])
+    kw = dict(t_mem=6.4, ae=5.0, temperature=4, threshold=1e-8, use_infinite=True)
+    p1 = ptgen_gpu.qd_phonon_pt_gpu(B, 0.1, **kw)
+    assert p1.meta["K"] == 65 and p1.meta["converged"]
+    p2 = ptgen_gpu.qd_phonon_pt_gpu(B, 0.1, K=130, **kw)
+    p3 = ptgen_gpu.qd_phonon_pt_gpu(B, 0.1, tail="svd", **kw)
+    rng = np.random.default_rng(2)
+    short = [rng.integers(0, 4, size=rng.integers(1, 141)) for _ in range(200)]
+    a, b = influence(p1, short), influence(p2, short)
+    d_short = np.max(np.abs(a - b)) / np.max(np.abs(b))
+    long_ = [rng.integers(0, 4, size=rng.integers(141, 401)) for _ in range(100)]
+    a, b, c = influence(p1, long_), influence(p2, long_), influence(p3, long_)
+    d_long = np.max(np.abs(a - b)) / np.max(np.abs(b))
+    d_noise = np.max(np.abs(a - c)) / np.max(np.abs(c))
+    print(f"K 65 vs 130: max influence difference {d_short:.2e} (<= 140 steps), {d_long:.2e} (<= 400 steps); "
+          f"QRCP vs SVD tail at K 65: {d_noise:.2e} (threshold 1e-8)")
+    assert d_short <= 10 * 1e-8
+    assert d_long <= 2 * d_noise + 1e-8
+
+
+def test_engine_refuses_pt_of_another_dt():
+    """engine.propagate raises on a PT generated for another dt before anything is launched"""
+    pt = ptgen.build_gaussian_pt(np.diag([0.0, 1.0]), 0.5, *ptgen.eta_coefficients(QDJ, 4.0, 0.5, 2), threshold=1e-8)
+    with pytest.raises(ValueError, match="dt = 0.5"):
+        engine.propagate(System(dim=2, H0=np.zeros((2, 2))), Grid(0.0, 0.1, 10), np.eye(2) / 2, [np.eye(2)],
+                         Trajectories(np.array([0]), np.array([10])), pt=pt)
+
+
+def test_ptg_scratch_per_stream_and_convergence_on_last_sweep():
+    """factorizations queued on two streams at once use separate scratch (a plain QR returns with its
+    kernels still queued), and a Jacobi that converges on its last allowed sweep is not reported as a failure"""
+    from pyaceqd_amd import ptgen_gpu, _lib
+    torch = _torch()
+    rng = np.random.default_rng(11)
+    A1, A2 = _rand(rng, 700, 300), _rand(rng, 500, 200)
+    s1 = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s1):
+        W1 = _dev(A1.T)
+        Q1, R1, _, k1 = ptgen_gpu.qr_cols(W1)
+    W2 = _dev(A2.T)
+    Q2, R2, _, k2 = ptgen_gpu.qr_cols(W2)                 # default stream, while s1's kernels may still run
+    torch.cuda.synchronize()
+    for A, Q, R in ((A1, Q1, R1), (A2, Q2, R2)):
+        Qh, Rh = Q.cpu().numpy().T, R.cpu().numpy().T
+        assert np.max(np.abs(Qh @ Rh - A)) < 1e-12 * np.max(np.abs(A)) * 30
+    X = _rand(rng, 96, 96)
+    ptgen_gpu.jacobi_cols(_dev(X.T), max_sweeps=60)
+    need = ptgen_gpu.LAST_SWEEPS
+    assert 2 <= need < 60
+    ptgen_gpu.jacobi_cols(_dev(X.T), max_sweeps=need)         # converges on its last allowed sweep
+    assert ptgen_gpu.LAST_SWEEPS == need
+    with pytest.raises(_lib.PQDError, match="no convergence"):
+        ptgen_gpu.jacobi_cols(_dev(X.T), max_sweeps=need - 1)

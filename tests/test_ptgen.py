@@ -109,7 +109,9 @@ def test_driver_generates_and_caches_pt(tmp_path, monkeypatch):
     name = str(tmp_path / ptgen.pt_cache_name("tls", 3.0, 4, "9", 0.5, 0.1, use_infinite=True)) + ".npz"
     assert os.path.isfile(name)
     pt2 = gs._resolve_pt(None, B, **kw)
-    assert np.array_equal(pt.Q, pt2.Q) and pt.n_init == 10
+    # use_infinite: the memory is the bath's own, bounded by the te = 2 t_mem horizon (20 steps here, not converged at
+    # a_e = 3 nm), not round(t_mem / dt) = 5
+    assert np.array_equal(pt.Q, pt2.Q) and pt.meta["K"] == 10 and pt.n_init == 20
     jf = str(tmp_path / "J.dat")
     gs._write_J(jf, 3.0, None, None)
     d = np.loadtxt(jf)
@@ -140,4 +142,135 @@ def test_driver_falls_back_when_ace_file_layout_unknown(tmp_path, monkeypatch):
         warnings.simplefilter("always")
         pt = gs._resolve_pt(None, B, **kw)
     assert any("not in a layout" in str(x.message) for x in w)
-    assert pt.n_init == 6 and os.path.isfile(name + ".npz")
+    assert pt.n_init == 12 and os.path.isfile(name + ".npz")   # use_infinite: K = 2 t_mem / dt = 6 (horizon)
+
+
+# ------------------------------------------------------------------ use_infinite and PT provenance
+def _influence(pt, paths):
+    out = []
+    for path in paths:
+        v = pt.bond0.copy()
+        s = 0
+        for n, a in enumerate(path):
+            s = n if n < pt.n_init else pt.n_init + (n - pt.n_init) % (pt.n_slices - pt.n_init)
+            v = v @ pt.Q[s, pt.gmap[a]]
+        out.append(v @ pt.closure[s])
+    return np.array(out)
+
+
+def test_infinite_memory_steps_rule():
+    """use_Gaussian_infinite (general_system.py:150-151, 165-167) takes the bath's own memory: the shortest K whose
+    neglected eta_k tail is below the threshold, bounded by the generate file's te = 2 t_mem horizon. The tls default
+    (tls.py:18: dt 0.1, a_e 5 nm, 4 K, threshold 1e-8) converges at K = 65 whatever t_mem; a_e = 3 nm keeps a ~1e-9
+    eta floor (the hard Boson_E_max cut of J) and takes the whole horizon."""
+    tls_B = np.diag([0.0, 1.0])
+    for tm in (6.4, 20.48):
+        _, _, info = ptgen.qd_phonon_eta(tls_B, 0.1, tm, 5.0, 4, 1e-8, use_infinite=True)
+        assert info["K"] == 65 and info["converged"]
+    _, _, info = ptgen.qd_phonon_eta(np.diag([0.0, 1, 1, 2]), 0.5, 20.48, 3.0, 4, 1e-10, use_infinite=True)
+    assert info["K"] == 82 and not info["converged"]
+    _, _, info = ptgen.qd_phonon_eta(tls_B, 0.1, 6.4, 5.0, 4, 1e-8, use_infinite=False)
+    assert info["K"] == 64
+    # the rule itself: the tail beyond K is below the threshold, the tail beyond K - 1 is not
+    eta, _, _ = ptgen.qd_phonon_eta(tls_B, 0.1, 6.4, 5.0, 4, 1e-8, K=128)
+    a = np.abs(eta)
+    assert a[66:].sum() <= 1e-8 < a[65:].sum()
+
+
+def test_infinite_memory_pt_converged_in_memory():
+    """the use_infinite PT does not change when its memory is doubled: influence values of 300 random paths (up to
+    6 K steps, explicit and repeated slices) agree to <= 10 x threshold (measured 3e-3 x threshold), while a
+    memory cut at K / 3 (what a short t_mem gives) moves them by > 100 x threshold"""
+    B, dt, thr = np.diag([0.0, 1.0]), 0.5, 1e-8
+    kw = dict(t_mem=20.48, ae=5.0, temperature=4, threshold=thr, use_infinite=True)
+    p1 = ptgen.qd_phonon_pt(B, dt, **kw)
+    K = p1.meta["K"]
+    assert p1.meta["converged"] and 10 <= K <= 20
+    p2 = ptgen.qd_phonon_pt(B, dt, K=2 * K, **kw)
+    p3 = ptgen.qd_phonon_pt(B, dt, K=K // 3, **kw)
+    rng = np.random.default_rng(0)
+    paths = [rng.integers(0, 4, size=rng.integers(1, 6 * K)) for _ in range(300)]
+    a, b, c = _influence(p1, paths), _influence(p2, paths), _influence(p3, paths)
+    assert np.max(np.abs(a - b)) <= 10 * thr * np.max(np.abs(b))
+    assert np.max(np.abs(c - b)) > 100 * thr * np.max(np.abs(b))
+
+
+def _kw(tmp_path, **over):
+    kw = dict(dt=0.5, t_mem=2.0, ae=5.0, temperature=4, threshold="7", factor_ah=None, boson_e_max=7, J_file=None,
+              J_to_file=None, use_infinite=True, system_prefix="tls", temp_dir=str(tmp_path) + os.sep, verbose=False)
+    kw.update(over)
+    return kw
+
+
+def test_cached_pt_regenerated_when_parameters_differ(tmp_path, monkeypatch):
+    """the reference's use_infinite cache name leaves out a_e (general_system.py:150-151): a second call at another
+    a_e finds the first call's file. Its stored generation parameters differ, so it is regenerated (with a warning)
+    and replaced; a third call at the same parameters reuses it silently"""
+    import warnings
+    monkeypatch.setenv("PQD_PTGEN", "host")
+    from pyaceqd_amd.general_system import general_system as gs
+    B = np.diag([0.0, 1.0]).astype(complex)
+    p5 = gs._resolve_pt(None, B, **_kw(tmp_path, ae=5.0))
+    assert p5.meta["ae"] == 5.0 and p5.meta["generator"] == "host" and p5.meta["dt"] == 0.5
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        p4 = gs._resolve_pt(None, B, **_kw(tmp_path, ae=4.0))
+    assert any("regenerating" in str(x.message) and "'ae'" in str(x.message) for x in w)
+    path = [np.full(12, 2)]
+    assert p4.meta["ae"] == 4.0 and abs(_influence(p4, path)[0] - _influence(p5, path)[0]) > 1e-3
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        p4b = gs._resolve_pt(None, B, **_kw(tmp_path, ae=4.0))
+    assert not w and np.array_equal(p4b.Q, p4.Q)
+    # the bond cap and the threshold are part of the key as well
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        gs._resolve_pt(None, B, **_kw(tmp_path, ae=4.0, threshold="8"))
+    assert not any("regenerating" in str(x.message) for x in w)     # another threshold has another file name
+    from pyaceqd_amd.pt import load_pt, save_pt
+    name = [f for f in os.listdir(tmp_path) if f.endswith("th7_dt0.5.pt.npz")][0]
+    p = load_pt(str(tmp_path / name))
+    p.meta["max_bond"] = 64
+    save_pt(str(tmp_path / name), p, dim=2)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        gs._resolve_pt(None, B, **_kw(tmp_path, ae=4.0))
+    assert any("regenerating" in str(x.message) and "max_bond" in str(x.message) for x in w)
+
+
+def test_pt_dt_and_dimension_mismatch_raise(tmp_path, monkeypatch):
+    """a PT generated at dt = 0.5 handed to a dt = 0.1 run, or a two-level PT to a four-level run, is an error
+    (ValueError), whether named explicitly, found in the cache or passed as an object"""
+    monkeypatch.setenv("PQD_PTGEN", "host")
+    from pyaceqd_amd.general_system import general_system as gs
+    from pyaceqd_amd.pt import save_pt
+    B = np.diag([0.0, 1.0]).astype(complex)
+    p = gs._resolve_pt(None, B, **_kw(tmp_path))
+    f = str(tmp_path / "mine.npz")
+    save_pt(f, p, dim=2)
+    with pytest.raises(ValueError, match="dt = 0.5"):
+        gs._resolve_pt(f, B, **_kw(tmp_path, dt=0.1))
+    with pytest.raises(ValueError, match="dt = 0.5"):
+        gs._resolve_pt(p, B, **_kw(tmp_path, dt=0.1))
+    with pytest.raises(ValueError, match="Liouville rows"):
+        gs._resolve_pt(f, np.diag([0.0, 1, 1, 2]).astype(complex), **_kw(tmp_path))
+    # explicitly named: used as given even when the stored parameters differ (the reference uses a given pt_file)
+    import warnings
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        q = gs._resolve_pt(f, B, **_kw(tmp_path, ae=3.0))
+    assert np.array_equal(q.Q, p.Q) and any("used as given" in str(x.message) for x in w)
+
+
+def test_explicit_unreadable_ace_file_raises(tmp_path, monkeypatch):
+    """an explicitly named ACE PT (`<pt_file>_initial`) in a layout this reader does not know is an error: it may
+    hold another bath, so no PT is generated in its place; under the automatic name the driver warns and
+    generates (test_driver_falls_back_when_ace_file_layout_unknown)"""
+    monkeypatch.setenv("PQD_PTGEN", "host")
+    from pyaceqd_amd.general_system import general_system as gs
+    name = str(tmp_path / "user_pt")
+    for suf in ("_initial", "_initial_0", "_repeated", "_repeated_0"):
+        with open(name + suf, "wb") as f:
+            f.write(b"\x00\x01not a layout this reader knows\n")
+    with pytest.raises(ValueError, match="named explicitly"):
+        gs._resolve_pt(name, np.diag([0.0, 1.0]).astype(complex), **_kw(tmp_path))
