@@ -30,8 +30,10 @@ PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 (vector == matrix on gfx950), spec
 PEAK_HBM_GBS = 8000.0
 
 
-def build_workload(n_t1, n_tau, chi, scan=1, scan_offset=0, dt=0.1, seed=1234, dictionary=False, t1_offset=0):
-    """(systems, grid, pt, rho0, ops, traj): `scan` pulse-area points x `n_t1` t1 points (t1 steps t1_offset ...)"""
+def build_workload(n_t1, n_tau, chi, scan=1, scan_offset=0, dt=0.1, seed=1234, dictionary=False, t1_offset=0,
+                   make_pt=True):
+    """(systems, grid, pt, rho0, ops, traj): `scan` pulse-area points x `n_t1` t1 points (t1 steps t1_offset ...);
+    make_pt=False leaves the synthetic PT out (pt = None: the caller brings its own)"""
     from pyaceqd_amd import engine, opgrammar, pt as ptmod
     from pyaceqd_amd.constants import hbar
     from pyaceqd_amd.four_level_system.linear import biexciton_ops
@@ -54,7 +56,7 @@ def build_workload(n_t1, n_tau, chi, scan=1, scan_offset=0, dt=0.1, seed=1234, d
         systems.append(engine.System(dim=N, H0=H0, lindblad=lind, channels=chans, sample_t0=0.0, sample_dt=ds))
     grid = engine.Grid(0.0, dt, n_steps, 1)
     pt = ptmod.synthetic_pt(mat(bo), chi=chi, n_init=min(410, n_steps), n_rep=1, seed=seed, eps=0.05, dt=dt,
-                            dictionary=dictionary)
+                            dictionary=dictionary) if make_pt else None
     A, B, Cm = mat("|3><1|_4"), mat("|1><1|_4"), mat("|1><3|_4")
     mtos, beg, end, sysidx = [], [], [], []
     for k in range(scan):

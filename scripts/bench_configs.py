@@ -13,6 +13,11 @@ algorithmic flops (fused half steps: F = 8 (D chi^2 + chi N^4 + n_out N^2), D = 
   c4reuse G2_reuse-shaped biexciton sweep (reference pol_entanglement/G2.py:486-497): 8 scan points x 1024 t1 points
           spread over [0, tend), every trajectory from step 0 to tend = 4,096 steps with its MTOs at t1, chi = 64;
           run without (PQD_BRANCH=0) and with shared trunks: executed vs useful traj-steps and wall per launch
+  c4d128  the bench workload (8 scan points x 256 t1 x 10,000 tau, biexciton) on a synthetic chi = 128 dictionary PT
+          (9 slices for the 16 rows: the shape of a generated biexciton PT at the reference parameters)
+  c4g     the same workload on a GPU-generated biexciton PT at dt = 0.1 and the reference's biexciton parameters
+          (four_level_system/linear.py: t_mem 20.48 -> K = 205, a_e 3 nm, 4 K, threshold 1e-10, bond cap 128): the
+          workload the drop-in produces with phonons; c4g2k: n_tau = 2,000
   c5dm    C5 as specified: sixls_linear + polarisation-entanglement tomography (calc_densitymatrix_reuse) over an
           e0 x bx grid (2 x {0, 1, 2, 4} points, tests/six_level_linear.py pulse pair, tend 400 ps, dt 0.1 ps, the
           class's t1 grid, chi = 64 dictionary PT), three launches for the whole grid (densitymatrix_reuse_scan)
@@ -39,7 +44,22 @@ def _xy(p, t):
     return p.polar_x * f, p.polar_y * f
 
 
-def workload(model, n_scan, n_t1, n_tau, chi, dt=0.1, dictionary=False):
+GEN = {}  # generated PTs of this process (c4g, c4g2k share one)
+
+
+def generated_pt(bo_mat, dt, K=None):
+    """the biexciton PT at the reference's parameters (four_level_system/linear.py:8: t_mem 20.48, a_e 3, 4 K,
+    threshold 10), generated on the GPU; K overrides the memory (shorter runs)"""
+    from pyaceqd_amd import ptgen_gpu
+    key = (dt, K)
+    if key not in GEN:
+        t0 = time.perf_counter()
+        pt = ptgen_gpu.qd_phonon_pt_gpu(bo_mat, dt, t_mem=20.48, ae=3.0, temperature=4, threshold=1e-10, K=K)
+        GEN[key] = (pt, time.perf_counter() - t0)
+    return GEN[key]
+
+
+def workload(model, n_scan, n_t1, n_tau, chi, dt=0.1, dictionary=False, generated=False, gen_K=None):
     from pyaceqd_amd import engine, opgrammar, pt as ptmod
     from pyaceqd_amd.constants import hbar
     from pyaceqd_amd.pulses import ChirpedPulse, PulseTrain
@@ -83,7 +103,9 @@ def workload(model, n_scan, n_t1, n_tau, chi, dt=0.1, dictionary=False):
         systems.append(engine.System(dim=N, H0=H0, lindblad=lind, channels=chans, sample_t0=0.0, sample_dt=ds))
     grid = engine.Grid(0.0, dt, n_steps, 1)
     pt = None
-    if chi > 1:
+    if generated:
+        pt, _ = generated_pt(mat(bo), dt, gen_K)
+    elif chi > 1:
         pt = ptmod.synthetic_pt(mat(bo), chi=chi, n_init=min(410, n_steps), n_rep=1, seed=1234, eps=0.05, dt=dt,
                                dictionary=dictionary)
     mtos, beg, end, sysidx = [], [], [], []
@@ -115,6 +137,10 @@ CONFIGS = {
     "c5": dict(model="sixls", n_scan=32, n_t1=64, n_tau=2000, chi=64),
     "c5d": dict(model="sixls", n_scan=32, n_t1=64, n_tau=2000, chi=64, dictionary=True),
     "c3d": dict(model="biexciton", n_scan=8, n_t1=256, n_tau=2000, chi=64, dictionary=True),
+    "c4d128": dict(model="biexciton", n_scan=8, n_t1=256, n_tau=10000, chi=128, dictionary=True),
+    "c4d128s": dict(model="biexciton", n_scan=8, n_t1=256, n_tau=2000, chi=128, dictionary=True),
+    "c4g": dict(model="biexciton", n_scan=8, n_t1=256, n_tau=10000, chi=128, generated=True),
+    "c4g2k": dict(model="biexciton", n_scan=8, n_t1=256, n_tau=2000, chi=128, generated=True),
 }
 
 
@@ -135,12 +161,18 @@ def run(name, steps):
     res = plan.download()
     assert all(np.all(np.isfinite(r)) for r in res), "non-finite output"
     executed = int(np.sum(tr.out_end + 1))
-    chi = cfg["chi"]
+    chi = pt.chi if pt is not None else cfg["chi"]
+    extra = {}
+    if cfg.get("generated"):
+        _, gen_s = generated_pt(None, cfg.get("dt", 0.1), cfg.get("gen_K"))
+        extra = {"pt_chi": pt.chi, "pt_D": pt.D, "pt_slices": pt.n_slices, "pt_gen_s": gen_s,
+                 "pt_K": (pt.meta or {}).get("K")}
     F = 8 * (N * N * chi * chi + chi * N ** 4 + len(ops) * N * N) if chi > 1 else 8 * (N ** 4 + len(ops) * N * N)
     tf = executed * F / (ms_sweep * 1e-3) / 1e12
     return {"config": name, **cfg, "N": N, "n_traj": tr.n_traj, "executed_traj_steps": executed,
             "wall_ms_per_launch": el * 1e3, "pt_sweep_ms": ms_sweep, "free_prop_ms": ms_free,
-            "traj_steps_per_s": executed / el, "flop_per_traj_step": F, "sweep_TFLOPs": tf, "frac_fp64": tf / PEAK}
+            "traj_steps_per_s": executed / el, "flop_per_traj_step": F, "sweep_TFLOPs": tf, "frac_fp64": tf / PEAK,
+            **extra}
 
 
 def run_c4reuse(steps, n_scan=8, n_t1=1024, n_steps=4096, chi=64):

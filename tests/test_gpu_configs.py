@@ -255,6 +255,28 @@ def test_config4_g2_sweep_256_t1_structured_pt_is_bare_and_shards_are_exact():
             assert np.array_equal(part[k], a[lo + k]) or rel(part[k], a[lo + k]) < 1e-13
 
 
+def test_config4_generated_chi128_pt_full_length_vs_oracle_subgrid():
+    """the workload the drop-in produces with phonons: the C4 shape (8 scan points x 256 t1 x
+    10,000 tau steps, 2,048 trajectories) on a biexciton PT GENERATED on the GPU at dt = 0.1 with the reference's
+    bath parameters (a_e 3 nm, 4 K, threshold 1e-10, bond cap 128; memory 4.1 ps here instead of 20.48 to keep the
+    generation to seconds): chi = 128 and a 9-entry dictionary, so the sweep runs pt_sweep_kernel<16, 128, 4> with
+    dictionary PT units. 16 trajectories spread over every scan point against the oracle at full length."""
+    import bench
+    from pyaceqd_amd import ptgen_gpu
+    sysd, grid, _, rho0, ops, tr = bench.build_workload(256, 10000, 128, scan=8, make_pt=False)
+    B = opgrammar.to_matrix("1*(|1><1|_4 + |2><2|_4) + 2*|3><3|_4", 4)
+    pt = ptgen_gpu.qd_phonon_pt_gpu(B, 0.1, t_mem=4.1, ae=3.0, temperature=4, threshold=1e-10)
+    assert pt.chi == 128 and pt.D == 9 and pt.meta["K"] == 41
+    plan = engine.Plan(sysd, grid, rho0, ops, tr, pt=pt)
+    plan.execute()
+    got = plan.download()
+    assert len(got) == 2048 and got[0].shape == (10001, 2)
+    ids = np.arange(0, 2048, 128) + np.arange(16) % 7
+    ref = oracle.propagate(sysd, grid, rho0, ops, _subset(tr, ids), pt=pt, nthreads=16)
+    cmp_lists([got[i] for i in ids], ref, 1e-10)
+    assert max(abs(g[0, 1]) for g in got) > 0
+
+
 # ------------------------------------------------------------------------------------------------ config 5
 SX, SY = "|0><1|_6 + |1><5|_6", "|0><2|_6 + |2><5|_6"
 SXD, SYD = "|1><0|_6 + |5><1|_6", "|2><0|_6 + |5><2|_6"
