@@ -133,6 +133,20 @@ _SIGS = {
 EXPORTED = tuple(_SIGS)
 
 
+def _torch_runtime_first():
+    """One HIP runtime per process: torch's ROCm wheel bundles its own libamdhip64 under the soname libpqd links, and
+    whichever library loads first serves both. If libpqd came first, torch.cuda.is_available() turned False later in
+    the process (the GPU PT generator and the sharded scans use torch device tensors; seen when a process ran libpqd
+    propagations before its first generator call). Importing torch (no device initialisation) before libpqd makes
+    the order the working one in every process. PQD_TORCH_FIRST=0 skips it; without torch nothing changes."""
+    if os.environ.get("PQD_TORCH_FIRST", "1") == "0":
+        return
+    try:
+        import torch  # noqa: F401
+    except Exception:  # torch absent or broken: libpqd runs on its own runtime
+        pass
+
+
 def lib():
     """Load libpqd.so (raises PQDError if it is missing: there is no fallback)."""
     global _lib
@@ -141,6 +155,7 @@ def lib():
             if _lib is None:
                 if not os.path.exists(LIB_PATH):
                     raise PQDError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+                _torch_runtime_first()
                 L = C.CDLL(LIB_PATH)
                 for name, (args, res) in _SIGS.items():
                     if os.environ.get("PQD_LIB") and not hasattr(L, name):

@@ -73,7 +73,11 @@ struct SplitLayout {
     static constexpr int LDS = (LDS_STATE * 16 > SP_LDS_FORCE) ? LDS_STATE * 16 : SP_LDS_FORCE;
 };
 
-template <int N2, int CHI, bool GRAN>
+// diagnostics (PQD_ABLATE bit 32, scripts/split_stamps.py): s_memtime at the phase boundaries of steps 1000..1015 in
+// workgroups 0 and G-1 of trajectory 0 (thread 0): [wg 0 / 1][step][phase 0..7]
+__device__ unsigned long long g_split_stamps[2 * 16 * 8];
+
+template <int N2, int CHI, bool GRAN, bool STAMP = false>
 __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2* __restrict__ X,
                                                          unsigned* __restrict__ cnt, unsigned* __restrict__ err) {
     using L = SplitLayout<N2, CHI>;
@@ -181,7 +185,17 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
     if (n_end > 0) fetch_slice(0);
     int cur_slice = n_end > 0 ? p.sched[0] : -1;  // the slice index sreg holds
     bool pre = false;  // frow holds F(n)[g][tid] of the coming step
+    // phase stamps: 0 top, 1 column phase done, 2 PT partials in LDS, 3 row published + arrived, 4 output/prefetch
+    // done, 5 peers arrived (poll + barrier), 6 state gathered (end of step)
+    auto stamp = [&](int n, int k) {
+        if constexpr (STAMP) {
+            const int wsel = g == 0 ? 0 : (g == G - 1 ? 1 : -1);
+            if (t == 0 && wsel >= 0 && threadIdx.x == 0 && n >= 1000 && n < 1016)
+                g_split_stamps[(wsel * 16 + (n - 1000)) * 8 + k] = __builtin_amdgcn_s_memtime();
+        }
+    };
     for (int n = 0;; ++n) {
+        stamp(n, 0);
         // ---- trunk pre-pass: checkpoint of the state at the top of step n (M_b(n-1) still deferred), workgroup 0
         if (p.ck_map && g == 0 && n >= 1) {
             const int c = p.ck_map[(size_t)t * p.ck_stride + n];
@@ -223,12 +237,14 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
             apply_global(fw_M(p, sy, wn, 2 * n, m2));
             rb = qo + g * CHI;
         }
+        stamp(n, 1);
         // ---- PT row g: y = row . S(n) -> exchange buffer (parity n & 1)
         double2 acc = c_zero();
 #pragma unroll
         for (int j = 0; j < KPER; ++j) c_fma(acc, smem[rb + kq * KPER + j], sreg[j]);
         smem[REDO + tid] = acc;
         __syncthreads();
+        stamp(n, 2);
         if (GRAN) {
             // thread q publishes word (q & 3) of element q >> 2 (every thread one granule when CHI = 64)
             const unsigned ep = (unsigned)n + 1u;
@@ -254,6 +270,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
             __syncthreads();
             if (tid == 0) __hip_atomic_fetch_add((gu32*)ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        stamp(n, 3);
         // ---- prefetch the next step's slice row (only when the schedule changes the slice: the repeated slice of
         // ACE's _repeated / infinite PTs stays in registers) and fused operator row
         if (fz) output(n, fw_W(p, sy, wn, n, N2));  // off the group's critical path (workgroup 0 only)
@@ -263,6 +280,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         }
         pre = p.fuse && n + 1 < n_end && !has_event(n + 1);
         if (pre && tid < N2) frow = gld(fw_F(p, sy, wn, n + 1, m2) + (size_t)g * N2 + tid);
+        stamp(n, 4);
         if (GRAN) {
             // ---- sweep: every element of the state, 2 x 16-B sc1 loads (2 granules each), re-read until its four
             // tags are n + 1; each wave leaves when all its elements have arrived
@@ -322,21 +340,26 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
             }
             __syncthreads();
             if (s_abort) return;
+            stamp(n, 5);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: payload loads are sc1
             const double2* Xn = Xt + (size_t)(n & 1) * E;
             for (int e = tid; e < E; e += SP_NT) smem[qo + e] = ld_sc1(Xn + e);
             __syncthreads();
+            stamp(n, 6);
         }
     }
 }
 
-template <int N2, int CHI, bool GRAN>
+template <int N2, int CHI, bool GRAN, bool STAMP = false>
 hipError_t launch_split_tg(int n_traj, const SweepParams& p, double2* X, unsigned* cnt, unsigned* err, hipStream_t s) {
     using L = SplitLayout<N2, CHI>;
     static_assert(L::LDS <= 160 * 1024, "LDS budget");
+    if constexpr (!STAMP && !GRAN && N2 == 16 && CHI == 64) {
+        if (p.ablate & 32) return launch_split_tg<N2, CHI, GRAN, true>(n_traj, p, X, cnt, err, s);
+    }
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)pt_split_kernel<N2, CHI, GRAN>,
+        hipError_t e = hipFuncSetAttribute((const void*)pt_split_kernel<N2, CHI, GRAN, STAMP>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::LDS);
         if (e != hipSuccess) return e;
         attr = true;
@@ -351,7 +374,7 @@ hipError_t launch_split_tg(int n_traj, const SweepParams& p, double2* X, unsigne
         q.split_xcd = n_traj;
         nb = 8u * (unsigned)(per_slot * N2);
     }
-    hipLaunchKernelGGL((pt_split_kernel<N2, CHI, GRAN>), dim3(nb), dim3(SP_NT), L::LDS, s, q, X, cnt, err);
+    hipLaunchKernelGGL((pt_split_kernel<N2, CHI, GRAN, STAMP>), dim3(nb), dim3(SP_NT), L::LDS, s, q, X, cnt, err);
     return hipGetLastError();
 }
 
@@ -444,4 +467,9 @@ hipError_t launch_split(int N2, int CHI, int n_traj, const SweepParams& p, doubl
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+// diagnostics: the stamps of the last PQD_ABLATE=32 split launch (2 workgroups x 16 steps x 8 phase slots)
+extern "C" int pqd_debug_split_stamps(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_split_stamps), sizeof(unsigned long long) * 256) == hipSuccess ? 0 : 4;
 }
