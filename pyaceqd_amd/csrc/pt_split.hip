@@ -69,7 +69,8 @@ struct SplitLayout {
     static constexpr int KPER = CHI / KG;             // slice rows per thread
     static constexpr int RPT = (N2 + KG - 1) / KG;    // state rows per thread in the column phase
     static constexpr int OPER = (N2 * N2 + SP_NT - 1) / SP_NT;  // operator elements per thread (staging)
-    static constexpr int LDS_STATE = 2 * N2 * CHI + N2 * N2 + N2 + SP_NT;  // complex elements
+    static constexpr int WST = 4 * SP_NT;                     // output-row elements staged in LDS (n_out N2 <= WST)
+    static constexpr int LDS_STATE = 2 * N2 * CHI + N2 * N2 + N2 + SP_NT + CHI + WST;  // complex elements
     static constexpr int LDS = (LDS_STATE * 16 > SP_LDS_FORCE) ? LDS_STATE * 16 : SP_LDS_FORCE;
 };
 
@@ -85,8 +86,10 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
     constexpr int G = N2, E = N2 * CHI;
     extern __shared__ __attribute__((aligned(16))) double2 smem[];
     // smem: full state ping-pong [0, E) and [E, 2E), staged column operator, closure contractions r[beta]
-    // (output phase), PT partial sums — all indexed off smem so every access stays ds_*
-    constexpr int OPO = 2 * E, RRO = OPO + N2 * N2, REDO = RRO + N2;
+    // (output phase), PT partial sums, the step's closure vector and output rows (workgroup 0) — all indexed off
+    // smem so every access stays ds_*
+    constexpr int OPO = 2 * E, RRO = OPO + N2 * N2, REDO = RRO + N2, CVO = REDO + SP_NT, WRO = CVO + CHI;
+    constexpr int WST = L::WST, WPT = WST / SP_NT;
     __shared__ int s_abort;
     if (threadIdx.x == 0) s_abort = 0;
 
@@ -152,28 +155,71 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         }
         apply_lds();
     };
-    // output(n) through rows w[k][.] (ovec, or W(n) on the state before M_b(n-1)): workgroup 0 writes it
-    auto output = [&](int n, const double2* __restrict__ w) {
+    // phase stamps: 0 top, 1 column phase done, 2 PT partials in LDS, 3 row published + arrived, 4 output/prefetch
+    // done, 5 peers arrived (poll + barrier), 6 state gathered (end of step); 7 output operands staged (workgroup 0)
+    auto stamp = [&](int n, int k) {
+        if constexpr (STAMP) {
+            const int wsel = g == 0 ? 0 : (g == G - 1 ? 1 : -1);
+            if (t == 0 && wsel >= 0 && threadIdx.x == 0 && n >= 1000 && n < 1016)
+                g_split_stamps[(wsel * 16 + (n - 1000)) * 8 + k] = __builtin_amdgcn_s_memtime();
+        }
+    };
+    // output(n) through rows w[k][.] (ovec, or W(n) on the state before M_b(n-1)): workgroup 0 writes it. The closure
+    // vector and the rows are fetched into registers a step ahead (ofetch) and staged in LDS here, so the
+    // pass is LDS-only: it sits on the group's critical path every step (workgroup 0 publishes step n + 1 only after
+    // it), and with the loads inside it took ~6,500 of a ~12,800-cycle C3 step (profiles/r05/split/stamps_before.log)
+    double2 cvr = c_zero(), wrr[WPT];
+    bool wdirect = false;  // more output-row elements than the staging area: read them from memory in the pass
+    auto ofetch = [&](int n, const double2* __restrict__ w) {
         if (g != 0 || n < wb || n > we) return;
         const double2* cv = (n == 0) ? p.closure0 : p.closure + (size_t)p.sched[n - 1] * CHI;
+        if (tid < CHI) cvr = gld(cv + tid);
+        wdirect = p.n_out * N2 > WST;
+        if (!wdirect) {
+#pragma unroll
+            for (int i = 0; i < WPT; ++i) {
+                const int e = tid + SP_NT * i;
+                wrr[i] = e < p.n_out * N2 ? gld(w + e) : c_zero();
+            }
+        }
+    };
+    auto output = [&](int n, const double2* __restrict__ w) {
+        if (g != 0 || n < wb || n > we) return;
+        if (tid < CHI) smem[CVO + tid] = cvr;
+        if (!wdirect) {
+#pragma unroll
+            for (int i = 0; i < WPT; ++i)
+                if (tid + SP_NT * i < p.n_out * N2) smem[WRO + tid + SP_NT * i] = wrr[i];
+        }
         __syncthreads();
-        if (tid < 4 * N2) {
-            const int b = tid >> 2, q = tid & 3;
-            double2 s = c_zero();
-            for (int d = q; d < CHI; d += 4) c_fma(s, smem[qo + b * CHI + d], gld(cv + d));
-            s = c_add(s, c_shfl_xor(s, 1));
-            s = c_add(s, c_shfl_xor(s, 2));
-            if (q == 0) smem[RRO + b] = s;
+        stamp(n, 7);
+        // closure r[b] = sum_d Q[b][d] c[d]: QW lanes per row, all threads
+        constexpr int QW = N2 <= 16 ? 16 : 4;
+        constexpr int RPP = SP_NT / QW;  // rows per pass
+        const int q = tid % QW;
+        for (int b0 = 0; b0 < N2; b0 += RPP) {
+            const int b = b0 + tid / QW;
+            double2 sacc = c_zero();
+            if (b < N2)
+                for (int d = q; d < CHI; d += QW) c_fma(sacc, smem[qo + b * CHI + d], smem[CVO + d]);
+#pragma unroll
+            for (int m = 1; m < QW; m <<= 1) sacc = c_add(sacc, c_shfl_xor(sacc, m));
+            if (b < N2 && q == 0) smem[RRO + b] = sacc;
         }
         __syncthreads();
         for (int k = tid; k < p.n_out; k += SP_NT) {
-            double2 s = c_zero();
+            double2 sacc = c_zero();
 #pragma unroll
-            for (int b = 0; b < N2; ++b) c_fma(s, gld(w + (size_t)k * N2 + b), smem[RRO + b]);
-                    p.out[wo + (long long)(n - wb) * p.n_out + k] = s;
-                }
+            for (int b = 0; b < N2; ++b)
+                c_fma(sacc, wdirect ? gld(w + (size_t)k * N2 + b) : smem[WRO + k * N2 + b], smem[RRO + b]);
+            p.out[wo + (long long)(n - wb) * p.n_out + k] = sacc;
+        }
     };
-    auto has_event = [&](int n) { return ev_cur < ev_lim && p.ev[ev_cur].x == n; };
+    // the step of the next unconsumed event, kept in a register: the fast path asks it every step and a p.ev load there
+    // was a dependent memory round trip on the group's critical path (re-read only when an event is consumed)
+    int ev_next = ev_cur < ev_lim ? p.ev[ev_cur].x : INT_MAX;
+    auto has_event = [&](int n) { return ev_next == n; };
+    auto ev_advance = [&]() { ++ev_cur; ev_next = ev_cur < ev_lim ? p.ev[ev_cur].x : INT_MAX; };
 
     // slice row of PT(0) and row g of the fused operator of step 1
     double2 sreg[KPER], frow = c_zero();
@@ -183,17 +229,10 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         for (int j = 0; j < KPER; ++j) sreg[j] = gld(S + (size_t)(kq * KPER + j) * CHI + dcol);
     };
     if (n_end > 0) fetch_slice(0);
+    ofetch(0, p.ovec);  // step 0 is never fused
     int cur_slice = n_end > 0 ? p.sched[0] : -1;  // the slice index sreg holds
+    int sched_next = n_end > 1 ? p.sched[1] : -1;  // sched[n + 1], loaded a step ahead (off the critical path)
     bool pre = false;  // frow holds F(n)[g][tid] of the coming step
-    // phase stamps: 0 top, 1 column phase done, 2 PT partials in LDS, 3 row published + arrived, 4 output/prefetch
-    // done, 5 peers arrived (poll + barrier), 6 state gathered (end of step)
-    auto stamp = [&](int n, int k) {
-        if constexpr (STAMP) {
-            const int wsel = g == 0 ? 0 : (g == G - 1 ? 1 : -1);
-            if (t == 0 && wsel >= 0 && threadIdx.x == 0 && n >= 1000 && n < 1016)
-                g_split_stamps[(wsel * 16 + (n - 1000)) * 8 + k] = __builtin_amdgcn_s_memtime();
-        }
-    };
     for (int n = 0;; ++n) {
         stamp(n, 0);
         // ---- trunk pre-pass: checkpoint of the state at the top of step n (M_b(n-1) still deferred), workgroup 0
@@ -224,7 +263,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
                 const int4 ev = p.ev[ev_cur];
                 if (ev.x != n || ev.y != 0) break;
                 apply_global(p.sop + (size_t)ev.z * m2);
-                ++ev_cur;
+                ev_advance();
             }
             output(n, p.ovec);
             if (n >= n_end) break;
@@ -232,7 +271,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
                 const int4 ev = p.ev[ev_cur];
                 if (ev.x != n || ev.y != 1) break;
                 apply_global(p.sop + (size_t)ev.z * m2);
-                ++ev_cur;
+                ev_advance();
             }
             apply_global(fw_M(p, sy, wn, 2 * n, m2));
             rb = qo + g * CHI;
@@ -275,11 +314,17 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         // ACE's _repeated / infinite PTs stays in registers) and fused operator row
         if (fz) output(n, fw_W(p, sy, wn, n, N2));  // off the group's critical path (workgroup 0 only)
         if (n + 1 < n_end) {
-            const int ns = p.sched[n + 1];
+            const int ns = sched_next;
+            sched_next = n + 2 < n_end ? p.sched[n + 2] : -1;
             if (ns != cur_slice) { fetch_slice(n + 1); cur_slice = ns; }
         }
         pre = p.fuse && n + 1 < n_end && !has_event(n + 1);
         if (pre && tid < N2) frow = gld(fw_F(p, sy, wn, n + 1, m2) + (size_t)g * N2 + tid);
+        // the next step's output operands, a whole step ahead (W(n + 1) is a fresh row from memory every step)
+        if (n + 1 <= n_end) {
+            const bool fz1 = p.fuse && !has_event(n + 1);
+            ofetch(n + 1, fz1 ? fw_W(p, sy, wn, n + 1, N2) : p.ovec);
+        }
         stamp(n, 4);
         if (GRAN) {
             // ---- sweep: every element of the state, 2 x 16-B sc1 loads (2 granules each), re-read until its four

@@ -50,7 +50,10 @@ def main():
         for k, nm in enumerate(NAMES):
             print(f"  {nm:16s} {ph[:, k].mean():8.0f}   min {ph[:, k].min():6d}  max {ph[:, k].max():6d}")
         print(f"  {'(end -> next 0)':16s} {(s[1:, 0] - s[:-1, -1]).mean():8.0f}")
-    print("skew (workgroup 15 - workgroup 0) at each phase:", np.round((st[1, :, :7] - st[0, :, :7]).mean(axis=0)))
+    o = st[0]
+    if np.all(o[:, 7] > 0):
+        print(f"workgroup 0 output pass: operands staged + barrier {np.mean(o[:, 7] - o[:, 3]):.0f}, "
+              f"closure + traces + next fetch {np.mean(o[:, 4] - o[:, 7]):.0f}")
 
 
 if __name__ == "__main__":
