@@ -27,6 +27,28 @@ __device__ __forceinline__ void c_fma(double2& acc, double2 a, double2 b) {
 __device__ __forceinline__ double2 c_shfl_xor(double2 v, int m) {
     return make_double2(__shfl_xor(v.x, m), __shfl_xor(v.y, m));
 }
+// one DPP move of a double inside a 16-lane row (two 32-bit moves; no LDS round trip, unlike __shfl_xor's ds_bpermute)
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// sum over each group of W (4 or 16) consecutive lanes, left in every lane of the group with the same bits (each step
+// adds the same pair in either order): quad_perm [1,0,3,2], quad_perm [2,3,0,1], then row_half_mirror, row_mirror.
+// Every lane of the wave must be active.
+template <int W>
+__device__ __forceinline__ double2 c_group_sum(double2 v) {
+    static_assert(W == 4 || W == 16, "lane groups of 4 or 16");
+    v = c_add(v, make_double2(dpp_d<0xB1>(v.x), dpp_d<0xB1>(v.y)));
+    v = c_add(v, make_double2(dpp_d<0x4E>(v.x), dpp_d<0x4E>(v.y)));
+    if constexpr (W == 16) {
+        v = c_add(v, make_double2(dpp_d<0x141>(v.x), dpp_d<0x141>(v.y)));
+        v = c_add(v, make_double2(dpp_d<0x140>(v.x), dpp_d<0x140>(v.y)));
+    }
+    return v;
+}
 
 // ---------------------------------------------------------------------------------------------
 // kernel parameter blocks (passed by value)

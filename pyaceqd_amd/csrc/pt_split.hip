@@ -170,9 +170,9 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
     // it), and with the loads inside it took ~6,500 of a ~12,800-cycle C3 step (profiles/r05/split/stamps_before.log)
     double2 cvr = c_zero(), wrr[WPT];
     bool wdirect = false;  // more output-row elements than the staging area: read them from memory in the pass
-    auto ofetch = [&](int n, const double2* __restrict__ w) {
+    auto ofetch = [&](int n, const double2* __restrict__ w, int sp) {  // sp = sched[n - 1] (n >= 1)
         if (g != 0 || n < wb || n > we) return;
-        const double2* cv = (n == 0) ? p.closure0 : p.closure + (size_t)p.sched[n - 1] * CHI;
+        const double2* cv = (n == 0) ? p.closure0 : p.closure + (size_t)sp * CHI;
         if (tid < CHI) cvr = gld(cv + tid);
         wdirect = p.n_out * N2 > WST;
         if (!wdirect) {
@@ -193,26 +193,36 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         }
         __syncthreads();
         stamp(n, 7);
-        // closure r[b] = sum_d Q[b][d] c[d]: QW lanes per row, all threads
+        // closure r[b] = sum_d Q[b][d] c[d], then out[k] = sum_b W[k][b] r[b]: QW consecutive lanes per row or
+        // output, summed by DPP moves inside the lane group (c_group_sum), every thread busy
         constexpr int QW = N2 <= 16 ? 16 : 4;
-        constexpr int RPP = SP_NT / QW;  // rows per pass
+        constexpr int RPP = SP_NT / QW;  // rows (outputs) per pass
         const int q = tid % QW;
         for (int b0 = 0; b0 < N2; b0 += RPP) {
             const int b = b0 + tid / QW;
             double2 sacc = c_zero();
             if (b < N2)
-                for (int d = q; d < CHI; d += QW) c_fma(sacc, smem[qo + b * CHI + d], smem[CVO + d]);
 #pragma unroll
-            for (int m = 1; m < QW; m <<= 1) sacc = c_add(sacc, c_shfl_xor(sacc, m));
+                for (int d = q; d < CHI; d += QW) c_fma(sacc, smem[qo + b * CHI + d], smem[CVO + d]);
+            sacc = c_group_sum<QW>(sacc);
             if (b < N2 && q == 0) smem[RRO + b] = sacc;
         }
         __syncthreads();
-        for (int k = tid; k < p.n_out; k += SP_NT) {
+        for (int k0 = 0; k0 < p.n_out; k0 += RPP) {
+            const int k = k0 + tid / QW;
             double2 sacc = c_zero();
+            // two loops, not one with a select: a global load in the merged loop put an s_waitcnt vmcnt(0) (every
+            // outstanding store and prefetch) in front of the staged path's FMAs too
+            if (k < p.n_out) {
+                if (wdirect) {
+                    for (int b = q; b < N2; b += QW) c_fma(sacc, gld(w + (size_t)k * N2 + b), smem[RRO + b]);
+                } else {
 #pragma unroll
-            for (int b = 0; b < N2; ++b)
-                c_fma(sacc, wdirect ? gld(w + (size_t)k * N2 + b) : smem[WRO + k * N2 + b], smem[RRO + b]);
-            p.out[wo + (long long)(n - wb) * p.n_out + k] = sacc;
+                    for (int b = q; b < N2; b += QW) c_fma(sacc, smem[WRO + k * N2 + b], smem[RRO + b]);
+                }
+            }
+            sacc = c_group_sum<QW>(sacc);
+            if (k < p.n_out && q == 0) p.out[wo + (long long)(n - wb) * p.n_out + k] = sacc;
         }
     };
     // the step of the next unconsumed event, kept in a register: the fast path asks it every step and a p.ev load there
@@ -223,15 +233,25 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
 
     // slice row of PT(0) and row g of the fused operator of step 1
     double2 sreg[KPER], frow = c_zero();
-    auto fetch_slice = [&](int n) {
-        const double2* __restrict__ S = p.Q + ((size_t)p.sched[n] * p.D + p.gmap[g]) * CHI * CHI;
+    const int grow = p.gmap[g];
+    auto fetch_slice = [&](int si) {  // si = sched[n], from a register (a p.sched load here was a dependent round trip)
+        const double2* __restrict__ S = p.Q + ((size_t)si * p.D + grow) * CHI * CHI;
 #pragma unroll
         for (int j = 0; j < KPER; ++j) sreg[j] = gld(S + (size_t)(kq * KPER + j) * CHI + dcol);
     };
-    if (n_end > 0) fetch_slice(0);
-    ofetch(0, p.ovec);  // step 0 is never fused
-    int cur_slice = n_end > 0 ? p.sched[0] : -1;  // the slice index sreg holds
-    int sched_next = n_end > 1 ? p.sched[1] : -1;  // sched[n + 1], loaded a step ahead (off the critical path)
+    // the schedule, 64 entries at a time in a VGPR (lane i holds sched[64 c + i]) one chunk ahead, picked with
+    // v_readlane: a uniform p.sched[n] load in the loop compiles to a vector load + readfirstlane that waits
+    // (s_waitcnt vmcnt(0)) for every outstanding vector memory op where it is issued — on every workgroup's critical
+    // path each step
+    const int lane = tid & 63;
+    auto sched_chunk = [&](int c) {
+        const int i = 64 * c + lane;
+        return i < n_end ? *(const __attribute__((address_space(1))) int*)(p.sched + i) : -1;
+    };
+    int sch_cur = sched_chunk(0), sch_nxt = sched_chunk(1);
+    int cur_slice = n_end > 0 ? __builtin_amdgcn_readlane(sch_cur, 0) : -1;  // the slice index sreg holds (sched[n])
+    if (n_end > 0) fetch_slice(cur_slice);
+    ofetch(0, p.ovec, 0);  // step 0 is never fused
     bool pre = false;  // frow holds F(n)[g][tid] of the coming step
     for (int n = 0;; ++n) {
         stamp(n, 0);
@@ -311,19 +331,22 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         }
         stamp(n, 3);
         // ---- prefetch the next step's slice row (only when the schedule changes the slice: the repeated slice of
-        // ACE's _repeated / infinite PTs stays in registers) and fused operator row
-        if (fz) output(n, fw_W(p, sy, wn, n, N2));  // off the group's critical path (workgroup 0 only)
+        // ACE's _repeated / infinite PTs stays in registers), issued right after the arrive so its 64 KiB are in flight
+        // during workgroup 0's output pass rather than in front of the poll; then the fused operator row
+        const int sn = cur_slice;  // sched[n]
         if (n + 1 < n_end) {
-            const int ns = sched_next;
-            sched_next = n + 2 < n_end ? p.sched[n + 2] : -1;
-            if (ns != cur_slice) { fetch_slice(n + 1); cur_slice = ns; }
+            const int m = n + 1;
+            if ((m & 63) == 0) { sch_cur = sch_nxt; sch_nxt = sched_chunk((m >> 6) + 1); }
+            const int ns = __builtin_amdgcn_readlane(sch_cur, m & 63);
+            if (ns != cur_slice) { fetch_slice(ns); cur_slice = ns; }
         }
+        if (fz) output(n, fw_W(p, sy, wn, n, N2));  // workgroup 0 only; it publishes step n + 1 after this
         pre = p.fuse && n + 1 < n_end && !has_event(n + 1);
         if (pre && tid < N2) frow = gld(fw_F(p, sy, wn, n + 1, m2) + (size_t)g * N2 + tid);
         // the next step's output operands, a whole step ahead (W(n + 1) is a fresh row from memory every step)
         if (n + 1 <= n_end) {
             const bool fz1 = p.fuse && !has_event(n + 1);
-            ofetch(n + 1, fz1 ? fw_W(p, sy, wn, n + 1, N2) : p.ovec);
+            ofetch(n + 1, fz1 ? fw_W(p, sy, wn, n + 1, N2) : p.ovec, sn);
         }
         stamp(n, 4);
         if (GRAN) {
