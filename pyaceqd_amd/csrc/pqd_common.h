@@ -123,6 +123,7 @@ struct SweepParams {
     int trpre;               // 1: traces one lane per (trajectory, output, row), W rows fetched a step ahead
     int ablate;              // diagnostics only (PQD_ABLATE): 1 skip PT, 2 skip column phases, 4 skip outputs
     int split_gran;          // split groups: data-tagged granule exchange (PQD_SPLIT_GRAN=1; default 0: counter form)
+    int split_ow;            // split groups, counter form: one output workgroup per group (default 1; PQD_SPLIT_OW=0 off)
     unsigned* flags;         // bit 0: a non-finite output value (set by launch_check_finite at synchronize)
     unsigned spin_limit;     // split groups: polls before a wait for the peers times out (PQD_SPLIT_SPIN, tests)
     int traj_base;           // split groups: trajectory of group 0 (a batch run as several co-resident launches)
@@ -253,6 +254,8 @@ hipError_t launch_map_tail(int N2, const double2* M, const double2* X, int n_x, 
 hipError_t launch_tl_dynmap(const double2* dm, int n_maps, int n, double rcond, double2* out, hipStream_t s);
 int tl_dynmap_nmax();
 bool split_supported(int N2, int CHI, int n_traj, int n_cu);
+int split_group_size(int N2);  // workgroups per split group (N2, or N2 + 1 with the output workgroup)
+bool split_ow_env();
 int split_blocks_per_cu(int N2, int CHI);
 hipError_t launch_split(int N2, int CHI, int n_traj, const SweepParams& p, double2* X, unsigned* cnt,
                         unsigned* err, hipStream_t s, int chunk = 0);

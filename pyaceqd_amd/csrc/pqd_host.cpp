@@ -606,7 +606,7 @@ static int plan_trunks(pqd_plan* P, pqd_ctx* ctx, int n_sys, const std::vector<s
     const int mode = e ? atoi(e) : 1;
     // more trunks than the device holds as co-resident groups: consecutive launches of as many as fit (C5 tomography:
     // 8 six-level trunks = 288 workgroups on 256 CUs -> 7 + 1; a group steps ~7x faster than a batched block)
-    const int fit = bpc >= 1 ? (n_cu * bpc) / N2 : 0;
+    const int fit = bpc >= 1 ? (n_cu * bpc) / split_group_size(N2) : 0;
     P->tk_chunk = fit >= 1 && nt > fit ? fit : 0;
     P->tk_split = mode != 0 && N2 >= 9 && bpc >= 1 && fit >= 1 &&
                   split_supported(N2, CHI, std::min(nt, fit), n_cu * bpc) &&
@@ -830,7 +830,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
         const int bpc = (pt && mode != 0) ? split_blocks_per_cu(N2, P->CHI) : 0;
         // a batch just above what the device holds runs as consecutive co-resident launches (up to 4 at N2 >= 25,
         // 2 below: a group step is 3.6x / 2.4x faster than a batched block's)
-        const int fit = bpc >= 1 ? (n_cu * bpc) / N2 : 0;
+        const int fit = bpc >= 1 ? (n_cu * bpc) / split_group_size(N2) : 0;
         const int max_launches = N2 >= 25 ? 4 : 2;
         P->split = pt && mode != 0 && fit >= 1 && split_supported(N2, P->CHI, std::min(tr->n_traj, fit), n_cu * bpc) &&
                    tr->n_traj <= max_launches * fit && (mode == 2 || N2 >= 9);
@@ -1028,6 +1028,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     // exchange form: counter (default; with the XCD-grouped grid C3 runs 5.02 us per step against 5.33 for the granules,
     // profiles/r04/split/xcd/) or data-tagged granules (PQD_SPLIT_GRAN=1)
     { const char* b1 = getenv("PQD_SPLIT_GRAN"); sp.split_gran = (b1 && atoi(b1) == 1) ? 1 : 0; }
+    sp.split_ow = split_ow_env() ? 1 : 0;  // the output workgroup (pt_split.hip OWG); split_group_size agrees
     { const char* b2 = getenv("PQD_SPLIT_XCD"); sp.split_xcd = (b2 && atoi(b2) == 0) ? 0 : 1; }
     // polls of a split group's counter before the wait counts as a timeout (~0.1 s); PQD_SPLIT_SPIN overrides
     // it (tests provoke the batched fallback with 0)

@@ -1,4 +1,4 @@
-// pt_split.hip — latency path for small batches: ONE trajectory spread over G = N2 workgroups.
+// pt_split.hip — latency path for small batches: ONE trajectory spread over a group of G = N2 (+ 1) workgroups.
 //
 // The batched sweep (pt_sweep.hip) gives a trajectory one wave of one workgroup, so a single run
 // (SURVEY §8d C3 "biexciton, chi 64, 1 MI355X": one trajectory) streams the whole PT slice set
@@ -8,18 +8,23 @@
 // column phases (M_b(n-1), MTOs, outputs, M_a(n), or the fused F(n) = M_a(n) M_b(n-1)) mix rows, so
 // every workgroup gathers the whole state (N2 x chi, 16 KiB at C3) once per step and runs them
 // redundantly — ONE exchange per step instead of a row/column transpose pair.
-// Hand-off (round 4, default): data-tagged granules (cdna_hip_programming.md §6 Guideline 16 R2: "the data
-// IS the flag"). Every 32-bit word of the row a workgroup publishes travels as one naturally aligned 8-B
-// {tag = step + 1, word} granule written by ONE relaxed agent-scope atomic store (global_store_dwordx2 sc1);
-// the consumers sweep the whole state's granules with sc1 loads and re-read the ones whose tag is not yet
-// the step's, until every tag matches. No drain, no counter, no barrier between publishing and reading: the
-// round-3 form below cost a drain + counter add + poll + 16 KiB gather per step (C3 single run 5.6 us/step).
-// Round-3 form (PQD_SPLIT_GRAN=0, MI355X_MICROARCH.md § visibility "Valid forms" table row 1): payload stores
-// 8-B sc1 atomics, every storing wave drains with s_waitcnt vmcnt(0), a workgroup barrier, then ONE lane adds
-// to the group's monotonic counter; wave 0 polls it with relaxed sc1 loads, the other waves wait at a barrier,
-// and every payload load is an sc1 load — so no fences.
+// Hand-off (default): a group counter. Payload stores are 8-B sc1 atomics, every storing wave drains with
+// s_waitcnt vmcnt(0), a workgroup barrier, then ONE lane adds to the group's monotonic counter; wave 0 polls it with
+// relaxed sc1 loads, the other waves wait at a barrier, and every payload load is an sc1 load — so no fences
+// (MI355X_MICROARCH.md § visibility "Valid forms" table row 1). With the XCD-grouped grid it beat the granule form
+// below (C3 5.02 vs 5.33 us per step, profiles/r04/split/xcd/).
+// Output workgroup (default in the counter form, PQD_SPLIT_OW=0 off): the group gets one more workgroup, g = N2, that
+// owns no PT row. It gathers the state like its peers, writes the outputs and trunk checkpoints, and arrives at the
+// top of each step (it has read the previous slot); without it workgroup 0 ran the output pass between its publish
+// and its poll and every peer waited for it (C3 single run 34.7 -> 31.8 ms, profiles/r05/ow/).
+// Alternative (PQD_SPLIT_GRAN=1): data-tagged granules (cdna_hip_programming.md §6 Guideline 16 R2: "the data IS
+// the flag"). Every 32-bit word of the row a workgroup publishes travels as one naturally aligned 8-B
+// {tag = step + 1, word} granule written by ONE relaxed agent-scope atomic store (global_store_dwordx2 sc1); the
+// consumers sweep the whole state's granules with sc1 loads and re-read the ones whose tag is not yet the step's,
+// until every tag matches: no drain, no counter, no barrier between publishing and reading.
 // Either exchange buffer is double-buffered by step parity (a workgroup cannot publish step n+2 before every
-// peer has gathered step n: its step n+1 row depends on that gather). One workgroup per CU (the LDS request
+// peer has gathered step n: its step n+1 row depends on that gather; the output workgroup's arrival at step n+1
+// says it has gathered step n). One workgroup per CU (the LDS request
 // forces it) and at most n_cu workgroups (host check), so every workgroup is resident; every spin is bounded
 // and a timeout ends the kernel with an error word the host turns into PQD_ERR_HIP (then the batched kernel).
 // Semantics are the sweep's: step n applies M_b(n-1), applyBefore MTOs at n,
@@ -78,12 +83,17 @@ struct SplitLayout {
 // workgroups 0 and G-1 of trajectory 0 (thread 0): [wg 0 / 1][step][phase 0..7]
 __device__ unsigned long long g_split_stamps[2 * 16 * 8];
 
-template <int N2, int CHI, bool GRAN, bool STAMP = false>
+template <int N2, int CHI, bool GRAN, bool OWG, bool STAMP = false>
 __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2* __restrict__ X,
                                                          unsigned* __restrict__ cnt, unsigned* __restrict__ err) {
     using L = SplitLayout<N2, CHI>;
     constexpr int KG = L::KG, KPER = L::KPER, RPT = L::RPT, OPER = L::OPER;
-    constexpr int G = N2, E = N2 * CHI;
+    static_assert(!(OWG && GRAN), "the output workgroup takes part in the counter form only");
+    // OWG: one more workgroup per group, g = N2, owns no PT row: it writes the outputs (and trunk checkpoints) from the
+    // gathered state while the N2 row workgroups contract and publish the next step, so the output pass leaves the
+    // group's critical path (without it workgroup 0 ran it between its publish and its poll, and every peer waited)
+    constexpr int G = N2 + (OWG ? 1 : 0), E = N2 * CHI;
+    constexpr int OG = OWG ? N2 : 0;  // the workgroup that writes outputs and checkpoints
     extern __shared__ __attribute__((aligned(16))) double2 smem[];
     // smem: full state ping-pong [0, E) and [E, 2E), staged column operator, closure contractions r[beta]
     // (output phase), PT partial sums, the step's closure vector and output rows (workgroup 0) — all indexed off
@@ -104,6 +114,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         g = loc - (loc / G) * G;
         if (tl >= p.split_xcd) return;  // an unused block (before any shared state is touched)
     }
+    const bool ow = OWG && g == N2;
     const int t = p.traj_base + tl;
     const int wb = p.wbeg[t], we = p.wend[t];
     const long long wo = p.woff[t];
@@ -171,7 +182,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
     double2 cvr = c_zero(), wrr[WPT];
     bool wdirect = false;  // more output-row elements than the staging area: read them from memory in the pass
     auto ofetch = [&](int n, const double2* __restrict__ w, int sp) {  // sp = sched[n - 1] (n >= 1)
-        if (g != 0 || n < wb || n > we) return;
+        if (g != OG || n < wb || n > we) return;
         const double2* cv = (n == 0) ? p.closure0 : p.closure + (size_t)sp * CHI;
         if (tid < CHI) cvr = gld(cv + tid);
         wdirect = p.n_out * N2 > WST;
@@ -184,7 +195,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         }
     };
     auto output = [&](int n, const double2* __restrict__ w) {
-        if (g != 0 || n < wb || n > we) return;
+        if (g != OG || n < wb || n > we) return;
         if (tid < CHI) smem[CVO + tid] = cvr;
         if (!wdirect) {
 #pragma unroll
@@ -233,7 +244,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
 
     // slice row of PT(0) and row g of the fused operator of step 1
     double2 sreg[KPER], frow = c_zero();
-    const int grow = p.gmap[g];
+    const int grow = ow ? 0 : p.gmap[g];
     auto fetch_slice = [&](int si) {  // si = sched[n], from a register (a p.sched load here was a dependent round trip)
         const double2* __restrict__ S = p.Q + ((size_t)si * p.D + grow) * CHI * CHI;
 #pragma unroll
@@ -250,33 +261,40 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
     };
     int sch_cur = sched_chunk(0), sch_nxt = sched_chunk(1);
     int cur_slice = n_end > 0 ? __builtin_amdgcn_readlane(sch_cur, 0) : -1;  // the slice index sreg holds (sched[n])
-    if (n_end > 0) fetch_slice(cur_slice);
+    if (n_end > 0 && !ow) fetch_slice(cur_slice);
     ofetch(0, p.ovec, 0);  // step 0 is never fused
     bool pre = false;  // frow holds F(n)[g][tid] of the coming step
     for (int n = 0;; ++n) {
         stamp(n, 0);
         // ---- trunk pre-pass: checkpoint of the state at the top of step n (M_b(n-1) still deferred), workgroup 0
-        if (p.ck_map && g == 0 && n >= 1) {
+        if (p.ck_map && g == OG && n >= 1) {
             const int c = p.ck_map[(size_t)t * p.ck_stride + n];
             if (c >= 0)
                 for (int e = tid; e < E; e += SP_NT) p.ck[(size_t)c * E + e] = smem[qo + e];
         }
+        // the output workgroup arrives at the top of the step: it has gathered step n - 1, so the row workgroups may
+        // reuse that slot for step n + 1 once their poll of step n has seen this (the counter counts G per step)
+        if (ow && n < n_end && tid == 0)
+            __hip_atomic_fetch_add((gu32*)ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // ---- column phase
         const bool fz = p.fuse && n >= 1 && !has_event(n);
         int rb;  // row g of the state the PT contracts
         if (fz) {
             // only row g of F(n) Q is needed here; Q itself stays for the deferred output(n) through W(n)
             if (n >= n_end) { output(n, fw_W(p, sy, wn, n, N2)); break; }
-            if (tid < N2) smem[OPO + tid] = pre ? frow : gld(fw_F(p, sy, wn, n, m2) + (size_t)g * N2 + tid);
-            __syncthreads();
-            if (tid < CHI) {
-                double2 acc = c_zero();
+            rb = to;
+            if (!ow) {
+                if (tid < N2) smem[OPO + tid] = pre ? frow : gld(fw_F(p, sy, wn, n, m2) + (size_t)g * N2 + tid);
+                __syncthreads();
+                if (tid < CHI) {
+                    double2 acc = c_zero();
 #pragma unroll
-                for (int b = 0; b < N2; ++b) c_fma(acc, smem[OPO + b], smem[qo + b * CHI + tid]);
-                smem[to + g * CHI + tid] = acc;
+                    for (int b = 0; b < N2; ++b) c_fma(acc, smem[OPO + b], smem[qo + b * CHI + tid]);
+                    smem[to + g * CHI + tid] = acc;
+                }
+                __syncthreads();
+                rb = to + g * CHI;
             }
-            __syncthreads();
-            rb = to + g * CHI;
         } else {
             if (n > 0) apply_global(fw_M(p, sy, wn, 2 * (n - 1) + 1, m2));
             while (ev_cur < ev_lim) {  // applyBefore MTOs at n
@@ -298,36 +316,38 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         }
         stamp(n, 1);
         // ---- PT row g: y = row . S(n) -> exchange buffer (parity n & 1)
-        double2 acc = c_zero();
+        if (!ow) {
+            double2 acc = c_zero();
 #pragma unroll
-        for (int j = 0; j < KPER; ++j) c_fma(acc, smem[rb + kq * KPER + j], sreg[j]);
-        smem[REDO + tid] = acc;
-        __syncthreads();
-        stamp(n, 2);
-        if (GRAN) {
-            // thread q publishes word (q & 3) of element q >> 2 (every thread one granule when CHI = 64)
-            const unsigned ep = (unsigned)n + 1u;
-            for (int q = tid; q < 4 * CHI; q += SP_NT) {
-                const int el = q >> 2, wd = q & 3;
-                double2 y = smem[REDO + el];
-#pragma unroll
-                for (int kg = 1; kg < KG; ++kg) y = c_add(y, smem[REDO + kg * CHI + el]);
-                const double v = (wd < 2) ? y.x : y.y;
-                const unsigned word = (wd & 1) ? (unsigned)__double2hiint(v) : (unsigned)__double2loint(v);
-                st_granule(Gt + ((size_t)(n & 1) * E + (size_t)g * CHI + el) * 4 + wd, ep, word);
-            }
-        } else {
-            double2* Xn = Xt + (size_t)(n & 1) * E;
-            if (tid < CHI) {
-                double2 y = smem[REDO + tid];
-#pragma unroll
-                for (int q = 1; q < KG; ++q) y = c_add(y, smem[REDO + q * CHI + tid]);
-                st_sc1(Xn + (size_t)g * CHI + tid, y);
-            }
-            // ---- arrive (every storing wave drained, then one lane); the wait for the group is below
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            for (int j = 0; j < KPER; ++j) c_fma(acc, smem[rb + kq * KPER + j], sreg[j]);
+            smem[REDO + tid] = acc;
             __syncthreads();
-            if (tid == 0) __hip_atomic_fetch_add((gu32*)ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            stamp(n, 2);
+            if (GRAN) {
+                // thread q publishes word (q & 3) of element q >> 2 (every thread one granule when CHI = 64)
+                const unsigned ep = (unsigned)n + 1u;
+                for (int q = tid; q < 4 * CHI; q += SP_NT) {
+                    const int el = q >> 2, wd = q & 3;
+                    double2 y = smem[REDO + el];
+#pragma unroll
+                    for (int kg = 1; kg < KG; ++kg) y = c_add(y, smem[REDO + kg * CHI + el]);
+                    const double v = (wd < 2) ? y.x : y.y;
+                    const unsigned word = (wd & 1) ? (unsigned)__double2hiint(v) : (unsigned)__double2loint(v);
+                    st_granule(Gt + ((size_t)(n & 1) * E + (size_t)g * CHI + el) * 4 + wd, ep, word);
+                }
+            } else {
+                double2* Xn = Xt + (size_t)(n & 1) * E;
+                if (tid < CHI) {
+                    double2 y = smem[REDO + tid];
+#pragma unroll
+                    for (int q = 1; q < KG; ++q) y = c_add(y, smem[REDO + q * CHI + tid]);
+                    st_sc1(Xn + (size_t)g * CHI + tid, y);
+                }
+                // ---- arrive (every storing wave drained, then one lane); the wait for the group is below
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (tid == 0) __hip_atomic_fetch_add((gu32*)ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         stamp(n, 3);
         // ---- prefetch the next step's slice row (only when the schedule changes the slice: the repeated slice of
@@ -338,11 +358,14 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
             const int m = n + 1;
             if ((m & 63) == 0) { sch_cur = sch_nxt; sch_nxt = sched_chunk((m >> 6) + 1); }
             const int ns = __builtin_amdgcn_readlane(sch_cur, m & 63);
-            if (ns != cur_slice) { fetch_slice(ns); cur_slice = ns; }
+            if (ns != cur_slice) {
+                if (!ow) fetch_slice(ns);
+                cur_slice = ns;
+            }
         }
-        if (fz) output(n, fw_W(p, sy, wn, n, N2));  // workgroup 0 only; it publishes step n + 1 after this
+        if (fz) output(n, fw_W(p, sy, wn, n, N2));  // workgroup OG only (without OWG it publishes step n + 1 after this)
         pre = p.fuse && n + 1 < n_end && !has_event(n + 1);
-        if (pre && tid < N2) frow = gld(fw_F(p, sy, wn, n + 1, m2) + (size_t)g * N2 + tid);
+        if (pre && tid < N2 && !ow) frow = gld(fw_F(p, sy, wn, n + 1, m2) + (size_t)g * N2 + tid);
         // the next step's output operands, a whole step ahead (W(n + 1) is a fresh row from memory every step)
         if (n + 1 <= n_end) {
             const bool fz1 = p.fuse && !has_event(n + 1);
@@ -418,16 +441,16 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
     }
 }
 
-template <int N2, int CHI, bool GRAN, bool STAMP = false>
+template <int N2, int CHI, bool GRAN, bool OWG, bool STAMP = false>
 hipError_t launch_split_tg(int n_traj, const SweepParams& p, double2* X, unsigned* cnt, unsigned* err, hipStream_t s) {
     using L = SplitLayout<N2, CHI>;
     static_assert(L::LDS <= 160 * 1024, "LDS budget");
     if constexpr (!STAMP && !GRAN && N2 == 16 && CHI == 64) {
-        if (p.ablate & 32) return launch_split_tg<N2, CHI, GRAN, true>(n_traj, p, X, cnt, err, s);
+        if (p.ablate & 32) return launch_split_tg<N2, CHI, GRAN, OWG, true>(n_traj, p, X, cnt, err, s);
     }
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)pt_split_kernel<N2, CHI, GRAN, STAMP>,
+        hipError_t e = hipFuncSetAttribute((const void*)pt_split_kernel<N2, CHI, GRAN, OWG, STAMP>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::LDS);
         if (e != hipSuccess) return e;
         attr = true;
@@ -436,21 +459,24 @@ hipError_t launch_split_tg(int n_traj, const SweepParams& p, double2* X, unsigne
     // 8 slots x ceil(n_traj / 8) groups x G blocks, the blocks of missing groups return at once
     const int per_slot = (n_traj + 7) / 8;
     SweepParams q = p;
-    unsigned nb = (unsigned)(n_traj * N2);
+    constexpr int G = N2 + (OWG ? 1 : 0);
+    unsigned nb = (unsigned)(n_traj * G);
     q.split_xcd = 0;
-    if (p.split_xcd && per_slot * N2 <= 32) {
+    if (p.split_xcd && per_slot * G <= 32) {
         q.split_xcd = n_traj;
-        nb = 8u * (unsigned)(per_slot * N2);
+        nb = 8u * (unsigned)(per_slot * G);
     }
-    hipLaunchKernelGGL((pt_split_kernel<N2, CHI, GRAN, STAMP>), dim3(nb), dim3(SP_NT), L::LDS, s, q, X, cnt, err);
+    hipLaunchKernelGGL((pt_split_kernel<N2, CHI, GRAN, OWG, STAMP>), dim3(nb), dim3(SP_NT), L::LDS, s, q, X, cnt, err);
     return hipGetLastError();
 }
 
 template <int N2, int CHI>
 hipError_t launch_split_t(int n_traj, const SweepParams& p, double2* X, unsigned* cnt, unsigned* err, hipStream_t s) {
-    // p.split_gran (PQD_SPLIT_GRAN=1): data-tagged granule exchange; default 0 = the counter form
-    return p.split_gran ? launch_split_tg<N2, CHI, true>(n_traj, p, X, cnt, err, s)
-                        : launch_split_tg<N2, CHI, false>(n_traj, p, X, cnt, err, s);
+    // p.split_gran (PQD_SPLIT_GRAN=1): data-tagged granule exchange; default 0 = the counter form, with the output
+    // workgroup unless PQD_SPLIT_OW=0 (p.split_ow)
+    if (p.split_gran) return launch_split_tg<N2, CHI, true, false>(n_traj, p, X, cnt, err, s);
+    return p.split_ow ? launch_split_tg<N2, CHI, false, true>(n_traj, p, X, cnt, err, s)
+                      : launch_split_tg<N2, CHI, false, false>(n_traj, p, X, cnt, err, s);
 }
 
 template <int N2>
@@ -467,11 +493,11 @@ hipError_t launch_split_n(int CHI, int n_traj, const SweepParams& p, double2* X,
 template <int N2, int CHI>
 int split_occ_t() {
     using L = SplitLayout<N2, CHI>;
-    if (hipFuncSetAttribute((const void*)pt_split_kernel<N2, CHI, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void*)pt_split_kernel<N2, CHI, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)L::LDS) != hipSuccess)
         return 0;
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, pt_split_kernel<N2, CHI, false>, SP_NT, L::LDS) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, pt_split_kernel<N2, CHI, false, true>, SP_NT, L::LDS) != hipSuccess)
         return 0;
     return nb;
 }
@@ -488,6 +514,15 @@ int split_occ_n(int CHI) {
 
 }  // namespace
 
+// workgroups per group: the N2 row workgroups, plus the output workgroup in the counter form unless PQD_SPLIT_OW=0
+// (the same environment the plan's SweepParams.split_gran / split_ow are read from)
+bool split_ow_env() {
+    const char* g = getenv("PQD_SPLIT_GRAN");
+    const char* o = getenv("PQD_SPLIT_OW");
+    return !(g && atoi(g) == 1) && !(o && atoi(o) == 0);
+}
+int split_group_size(int N2) { return N2 + (split_ow_env() ? 1 : 0); }
+
 // workgroups of the split kernel the runtime can keep resident per CU (0: the kernel cannot run)
 int split_blocks_per_cu(int N2, int CHI) {
     switch (N2) {
@@ -503,7 +538,7 @@ int split_blocks_per_cu(int N2, int CHI) {
 bool split_supported(int N2, int CHI, int n_traj, int n_cu) {
     return (CHI == 16 || CHI == 32 || CHI == 64) &&
            (N2 == 4 || N2 == 9 || N2 == 16 || N2 == 25 || N2 == 36) && n_traj >= 1 &&
-           (long long)n_traj * N2 <= n_cu;
+           (long long)n_traj * split_group_size(N2) <= n_cu;
 }
 
 // X: n_traj * 4 * N2 * CHI double2 exchange buffer (granules, tags zeroed here); cnt: n_traj * 32 counters and err,
