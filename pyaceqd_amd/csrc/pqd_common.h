@@ -49,6 +49,26 @@ __device__ __forceinline__ double2 c_group_sum(double2 v) {
     }
     return v;
 }
+// x[l] + x[l ^ W] for W = 32 or 16 in every lane l, the same bits in both partners (each adds the same pair): gfx950's
+// v_permlane32_swap / v_permlane16_swap, one VALU move per 32-bit half instead of an LDS round trip. Whichever half
+// each swap moves, its two results hold x[l] and x[l ^ W] in some order, so their sum is the pair's.
+template <int W>
+__device__ __forceinline__ double xor_add(double x) {
+    static_assert(W == 32 || W == 16, "permlane swaps pair lanes 32 or 16 apart");
+    const long long b = __double_as_longlong(x);
+    const unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32);
+    unsigned l0, l1, h0, h1;
+    if constexpr (W == 32) {
+        const auto sl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+        const auto sh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+        l0 = sl[0]; l1 = sl[1]; h0 = sh[0]; h1 = sh[1];
+    } else {
+        const auto sl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+        const auto sh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+        l0 = sl[0]; l1 = sl[1]; h0 = sh[0]; h1 = sh[1];
+    }
+    return __longlong_as_double(((long long)h0 << 32) | l0) + __longlong_as_double(((long long)h1 << 32) | l1);
+}
 
 // ---------------------------------------------------------------------------------------------
 // kernel parameter blocks (passed by value)

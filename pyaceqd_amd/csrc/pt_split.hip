@@ -62,12 +62,6 @@ __device__ __forceinline__ void st_granule(unsigned long long* g, unsigned tag, 
     __hip_atomic_store((gu64*)g, ((unsigned long long)tag << 32) | word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ double2 ld_sc1(const double2* p) {
-    const unsigned long long x = __hip_atomic_load((gu64*)&p->x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long y = __hip_atomic_load((gu64*)&p->y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return make_double2(__longlong_as_double((long long)x), __longlong_as_double((long long)y));
-}
-
 template <int N2, int CHI>
 struct SplitLayout {
     static constexpr int KG = SP_NT / CHI;            // k groups of the row contraction
@@ -75,7 +69,7 @@ struct SplitLayout {
     static constexpr int RPT = (N2 + KG - 1) / KG;    // state rows per thread in the column phase
     static constexpr int OPER = (N2 * N2 + SP_NT - 1) / SP_NT;  // operator elements per thread (staging)
     static constexpr int WST = 4 * SP_NT;                     // output-row elements staged in LDS (n_out N2 <= WST)
-    static constexpr int LDS_STATE = 2 * N2 * CHI + N2 * N2 + N2 + SP_NT + CHI + WST;  // complex elements
+    static constexpr int LDS_STATE = 2 * N2 * CHI + N2 * N2 + N2 + 2 * SP_NT + CHI + WST;  // complex elements
     static constexpr int LDS = (LDS_STATE * 16 > SP_LDS_FORCE) ? LDS_STATE * 16 : SP_LDS_FORCE;
 };
 
@@ -99,6 +93,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
     // (output phase), PT partial sums, the step's closure vector and output rows (workgroup 0) — all indexed off
     // smem so every access stays ds_*
     constexpr int OPO = 2 * E, RRO = OPO + N2 * N2, REDO = RRO + N2, CVO = REDO + SP_NT, WRO = CVO + CHI;
+    constexpr int PRT = WRO + L::WST;  // counter form: KG partial sums of the next PT row (see the gather)
     constexpr int WST = L::WST, WPT = WST / SP_NT;
     __shared__ int s_abort;
     if (threadIdx.x == 0) s_abort = 0;
@@ -244,6 +239,25 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
 
     // slice row of PT(0) and row g of the fused operator of step 1
     double2 sreg[KPER], frow = c_zero();
+    // gather layout (counter form): slot i of thread tid holds state element ge(i), -1 past the state. chi = 64: wave w
+    // takes the columns 16 w .. 16 w + 15 of every row (its own PT k-range), lane group lane >> 4 the rows
+    // lane >> 4 + 4 i; otherwise element tid + SP_NT i
+    constexpr int EPT_G = (E + SP_NT - 1) / SP_NT;
+    const int lane = tid & 63;
+    auto ge = [&](int i) -> int {
+        if constexpr (CHI == 64) {
+            const int b = (lane >> 4) + 4 * i;
+            return b < N2 ? b * CHI + 16 * (tid >> 6) + (lane & 15) : -1;
+        } else {
+            const int e = tid + SP_NT * i;
+            return e < E ? e : -1;
+        }
+    };
+    // counter form, row workgroups: F(n + 1)[g][b] of the thread's gather elements (b = ge(i) / CHI): the gather of
+    // step n contracts them with the state as it arrives, so a fused step has no column phase
+    double2 fr[EPT_G];
+#pragma unroll
+    for (int i = 0; i < EPT_G; ++i) fr[i] = c_zero();
     const int grow = ow ? 0 : p.gmap[g];
     auto fetch_slice = [&](int si) {  // si = sched[n], from a register (a p.sched load here was a dependent round trip)
         const double2* __restrict__ S = p.Q + ((size_t)si * p.D + grow) * CHI * CHI;
@@ -254,7 +268,6 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
     // v_readlane: a uniform p.sched[n] load in the loop compiles to a vector load + readfirstlane that waits
     // (s_waitcnt vmcnt(0)) for every outstanding vector memory op where it is issued — on every workgroup's critical
     // path each step
-    const int lane = tid & 63;
     auto sched_chunk = [&](int c) {
         const int i = 64 * c + lane;
         return i < n_end ? *(const __attribute__((address_space(1))) int*)(p.sched + i) : -1;
@@ -263,7 +276,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
     int cur_slice = n_end > 0 ? __builtin_amdgcn_readlane(sch_cur, 0) : -1;  // the slice index sreg holds (sched[n])
     if (n_end > 0 && !ow) fetch_slice(cur_slice);
     ofetch(0, p.ovec, 0);  // step 0 is never fused
-    bool pre = false;  // frow holds F(n)[g][tid] of the coming step
+    bool pre = false;  // the coming step is fused: frow (granule form) / fr (counter form) hold its F row
     for (int n = 0;; ++n) {
         stamp(n, 0);
         // ---- trunk pre-pass: checkpoint of the state at the top of step n (M_b(n-1) still deferred), workgroup 0
@@ -283,7 +296,9 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
             // only row g of F(n) Q is needed here; Q itself stays for the deferred output(n) through W(n)
             if (n >= n_end) { output(n, fw_W(p, sy, wn, n, N2)); break; }
             rb = to;
-            if (!ow) {
+            // counter form: the gather of step n - 1 left row g of F(n) Q in PRT (pre was set): chi = 64 as the row
+            // itself (each wave wrote its own k-range), else as KG partial sums
+            if (!ow && GRAN) {
                 if (tid < N2) smem[OPO + tid] = pre ? frow : gld(fw_F(p, sy, wn, n, m2) + (size_t)g * N2 + tid);
                 __syncthreads();
                 if (tid < CHI) {
@@ -318,8 +333,22 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         // ---- PT row g: y = row . S(n) -> exchange buffer (parity n & 1)
         if (!ow) {
             double2 acc = c_zero();
+            if (!GRAN && fz && CHI == 64) {
 #pragma unroll
-            for (int j = 0; j < KPER; ++j) c_fma(acc, smem[rb + kq * KPER + j], sreg[j]);
+                for (int j = 0; j < KPER; ++j) c_fma(acc, smem[PRT + kq * KPER + j], sreg[j]);
+            } else if (!GRAN && fz) {
+#pragma unroll
+                for (int j = 0; j < KPER; ++j) {
+                    const int k = kq * KPER + j;
+                    double2 r = smem[PRT + k];
+#pragma unroll
+                    for (int kg = 1; kg < KG; ++kg) r = c_add(r, smem[PRT + kg * CHI + k]);
+                    c_fma(acc, r, sreg[j]);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < KPER; ++j) c_fma(acc, smem[rb + kq * KPER + j], sreg[j]);
+            }
             smem[REDO + tid] = acc;
             __syncthreads();
             stamp(n, 2);
@@ -365,7 +394,16 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         }
         if (fz) output(n, fw_W(p, sy, wn, n, N2));  // workgroup OG only (without OWG it publishes step n + 1 after this)
         pre = p.fuse && n + 1 < n_end && !has_event(n + 1);
-        if (pre && tid < N2 && !ow) frow = gld(fw_F(p, sy, wn, n + 1, m2) + (size_t)g * N2 + tid);
+        if (GRAN) {
+            if (pre && tid < N2 && !ow) frow = gld(fw_F(p, sy, wn, n + 1, m2) + (size_t)g * N2 + tid);
+        } else if (pre && !ow) {
+            const double2* __restrict__ Fr = fw_F(p, sy, wn, n + 1, m2) + (size_t)g * N2;
+#pragma unroll
+            for (int i = 0; i < EPT_G; ++i) {
+                const int e = ge(i);
+                fr[i] = e >= 0 ? gld(Fr + e / CHI) : c_zero();
+            }
+        }
         // the next step's output operands, a whole step ahead (W(n + 1) is a fresh row from memory every step)
         if (n + 1 <= n_end) {
             const bool fz1 = p.fuse && !has_event(n + 1);
@@ -433,9 +471,43 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
             if (s_abort) return;
             stamp(n, 5);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: payload loads are sc1
-            const double2* Xn = Xt + (size_t)(n & 1) * E;
-            for (int e = tid; e < E; e += SP_NT) smem[qo + e] = ld_sc1(Xn + e);
-            __syncthreads();
+            // every element's 16-B sc1 load in flight before the first use (buffer loads, not atomic ones: the compiler
+            // kept relaxed atomic loads in order and waited vmcnt(0) on each element, four L2 round trips in a row)
+            v4u32 xr[EPT_G];
+#pragma unroll
+            for (int i = 0; i < EPT_G; ++i) {
+                const int e = ge(i);
+                xr[i] = __builtin_amdgcn_raw_buffer_load_b128(rG, (int)(((size_t)(n & 1) * E + (e >= 0 ? e : 0)) * 16),
+                                                              0, 16);
+            }
+            auto xel = [&](int i) {
+                return make_double2(__hiloint2double((int)xr[i].y, (int)xr[i].x),
+                                    __hiloint2double((int)xr[i].w, (int)xr[i].z));
+            };
+            if (pre && !ow) {
+                // a fused step next: only row g of F(n + 1) Q is needed, y[d] = sum_b F[g][b] Q[b][d]
+                double2 part = c_zero();
+#pragma unroll
+                for (int i = 0; i < EPT_G; ++i)
+                    if (ge(i) >= 0) c_fma(part, fr[i], xel(i));
+                if constexpr (CHI == 64) {
+                    // the four lane groups hold the same columns: add them (permlane swaps); lanes 0..15 keep
+                    // y[16 w + lane], which only this wave's PT reads — no barrier
+                    part = make_double2(xor_add<32>(part.x), xor_add<32>(part.y));
+                    part = make_double2(xor_add<16>(part.x), xor_add<16>(part.y));
+                    if (lane < 16) smem[PRT + 16 * (tid >> 6) + lane] = part;
+                } else {
+                    // the thread's elements share the column d = tid % CHI (SP_NT is a multiple of CHI) and sit in
+                    // rows tid / CHI + KG i: PRT[tid] = partial (tid / CHI, d); the PT sums the KG partials
+                    smem[PRT + tid] = part;
+                    __syncthreads();
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < EPT_G; ++i)
+                    if (ge(i) >= 0) smem[qo + ge(i)] = xel(i);
+                __syncthreads();
+            }
             stamp(n, 6);
         }
     }

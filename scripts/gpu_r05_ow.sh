@@ -2,7 +2,7 @@
 # round 5: split groups with the output workgroup (G = N2 + 1): split parity tests, stamps with and without it,
 # C3/C5 single-run timing with and without it (PQD_SPLIT_OW=0)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
-O=gpurun_out/r05/ow
+O=gpurun_out/r05/${TAG:-ow}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_robustness.py -m gpu -q \
