@@ -612,7 +612,7 @@ static int plan_trunks(pqd_plan* P, pqd_ctx* ctx, int n_sys, const std::vector<s
                   split_supported(N2, CHI, std::min(nt, fit), n_cu * bpc) &&
                   nt <= (N2 >= 25 ? 4 : 2) * fit;  // launches in a row still beat one batched pass (§4.6 latencies)
     HIPCHK(P->tk_Xs.alloc((size_t)nt * 4 * N2 * CHI));  // split exchange: 2 slots of granules (pt_split.hip)
-    HIPCHK(P->tk_cnt.alloc((size_t)nt * 32));
+    HIPCHK(P->tk_cnt.alloc((size_t)nt * 64));  // split arrival flags: two 128-B lines per group
     HIPCHK(P->tk_err.alloc(4));
     (void)ctx;
     return PQD_OK;
@@ -1081,7 +1081,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     finalize_trunks(P);
     if (P->split) {
         HIPCHK(P->Xs.alloc((size_t)P->n_traj * 4 * N2 * P->CHI));  // split exchange: 2 slots of granules
-        HIPCHK(P->cnt.alloc((size_t)P->n_traj * 32));
+        HIPCHK(P->cnt.alloc((size_t)P->n_traj * 64));  // split arrival flags: two 128-B lines per group
         HIPCHK(P->err.alloc(4));
     }
     HIPCHK(hipStreamSynchronize(s));

@@ -121,7 +121,10 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
     unsigned long long* __restrict__ Gt = reinterpret_cast<unsigned long long*>(Xt);
     // descriptor over this trajectory's granules, from workgroup-uniform values only (16-B sc1 loads of 2 granules)
     const __amdgpu_buffer_rsrc_t rG = __builtin_amdgcn_make_buffer_rsrc(Xt, 0, 4 * E * 16, 0x00020000);
-    unsigned* ct = cnt + (size_t)t * 32;  // one 128-B line per group counter
+    // counter form: the group's arrival flags, one word per workgroup (flag g = steps workgroup g has published; the
+    // output workgroup's = steps it has gathered + 1), two 128-B lines per group. One word per producer instead of one
+    // shared counter: no serialised atomics at the L2, and wave 0 reads every flag with ONE load per poll
+    unsigned* ct = cnt + (size_t)t * 64;
     const int n_end = we;
     constexpr int m2 = N2 * N2;
     const int ev_lim = p.ev_start[t + 1];
@@ -189,15 +192,19 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
             }
         }
     };
-    auto output = [&](int n, const double2* __restrict__ w) {
-        if (g != OG || n < wb || n > we) return;
+    // the fetched operands into LDS: after the poll of the step before (the loads have landed; a barrier before
+    // output() makes them visible), so the pass itself has no staging wait or barrier
+    auto ostage = [&]() {
+        if (g != OG) return;
         if (tid < CHI) smem[CVO + tid] = cvr;
         if (!wdirect) {
 #pragma unroll
             for (int i = 0; i < WPT; ++i)
                 if (tid + SP_NT * i < p.n_out * N2) smem[WRO + tid + SP_NT * i] = wrr[i];
         }
-        __syncthreads();
+    };
+    auto output = [&](int n, const double2* __restrict__ w) {
+        if (g != OG || n < wb || n > we) return;
         stamp(n, 7);
         // closure r[b] = sum_d Q[b][d] c[d], then out[k] = sum_b W[k][b] r[b]: QW consecutive lanes per row or
         // output, summed by DPP moves inside the lane group (c_group_sum), every thread busy
@@ -276,6 +283,8 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
     int cur_slice = n_end > 0 ? __builtin_amdgcn_readlane(sch_cur, 0) : -1;  // the slice index sreg holds (sched[n])
     if (n_end > 0 && !ow) fetch_slice(cur_slice);
     ofetch(0, p.ovec, 0);  // step 0 is never fused
+    ostage();
+    __syncthreads();
     bool pre = false;  // the coming step is fused: frow (granule form) / fr (counter form) hold its F row
     for (int n = 0;; ++n) {
         stamp(n, 0);
@@ -288,7 +297,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         // the output workgroup arrives at the top of the step: it has gathered step n - 1, so the row workgroups may
         // reuse that slot for step n + 1 once their poll of step n has seen this (the counter counts G per step)
         if (ow && n < n_end && tid == 0)
-            __hip_atomic_fetch_add((gu32*)ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store((gu32*)(ct + g), (unsigned)n + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // ---- column phase
         const bool fz = p.fuse && n >= 1 && !has_event(n);
         int rb;  // row g of the state the PT contracts
@@ -375,7 +384,8 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
                 // ---- arrive (every storing wave drained, then one lane); the wait for the group is below
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
-                if (tid == 0) __hip_atomic_fetch_add((gu32*)ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (tid == 0)
+                    __hip_atomic_store((gu32*)(ct + g), (unsigned)n + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         stamp(n, 3);
@@ -453,12 +463,17 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
             }
             __syncthreads();
             if (s_abort) return;
+            ostage();  // visible to output(n + 1) after the column phase's barriers
         } else {
             if (tid < 64) {
-                const unsigned target = (unsigned)G * (unsigned)(n + 1);
+                const unsigned want = (unsigned)n + 1u;
                 unsigned spins = 0;
                 bool ok = true;
-                while (__hip_atomic_load((gu32*)ct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                for (;;) {
+                    const unsigned v = lane < G
+                                           ? __hip_atomic_load((gu32*)(ct + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                           : want;
+                    if (__all(v >= want)) break;
                     __builtin_amdgcn_s_sleep(1);
                     if (++spins > p.spin_limit) { ok = false; break; }
                 }
@@ -470,6 +485,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
             __syncthreads();
             if (s_abort) return;
             stamp(n, 5);
+            ostage();  // visible to output(n + 1) after the gather's barrier (or the PT's, chi = 64 fused rows)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: payload loads are sc1
             // every element's 16-B sc1 load in flight before the first use (buffer loads, not atomic ones: the compiler
             // kept relaxed atomic loads in order and waited vmcnt(0) on each element, four L2 round trips in a row)
@@ -613,12 +629,12 @@ bool split_supported(int N2, int CHI, int n_traj, int n_cu) {
            (long long)n_traj * split_group_size(N2) <= n_cu;
 }
 
-// X: n_traj * 4 * N2 * CHI double2 exchange buffer (granules, tags zeroed here); cnt: n_traj * 32 counters and err,
+// X: n_traj * 4 * N2 * CHI double2 exchange buffer (granules, tags zeroed here); cnt: n_traj * 64 arrival words and err,
 // zeroed here before every launch.
 // chunk > 0: at most `chunk` trajectories per launch (each launch's groups co-resident), launched one after the other
 hipError_t launch_split(int N2, int CHI, int n_traj, const SweepParams& p, double2* X, unsigned* cnt,
                         unsigned* err, hipStream_t s, int chunk) {
-    hipError_t e = hipMemsetAsync(cnt, 0, (size_t)n_traj * 32 * sizeof(unsigned), s);
+    hipError_t e = hipMemsetAsync(cnt, 0, (size_t)n_traj * 64 * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
     if (p.split_gran) {  // every granule tag 0: never a step's epoch (n + 1 >= 1)
         e = hipMemsetAsync(X, 0, (size_t)n_traj * 4 * N2 * CHI * sizeof(double2), s);
