@@ -123,8 +123,17 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
     const __amdgpu_buffer_rsrc_t rG = __builtin_amdgcn_make_buffer_rsrc(Xt, 0, 4 * E * 16, 0x00020000);
     // counter form: the group's arrival flags, one word per workgroup (flag g = steps workgroup g has published; the
     // output workgroup's = steps it has gathered + 1), two 128-B lines per group. One word per producer instead of one
-    // shared counter: no serialised atomics at the L2, and wave 0 reads every flag with ONE load per poll
+    // shared counter: no serialised atomics at the L2, and wave 0 reads every flag with ONE load per poll. A group of
+    // more than 32 workgroups (N2 = 36: 37) spans two XCDs and two lines of flags; there one monotonic counter (one
+    // add per arrival, G per step) measured faster (C5 single run 43.1 -> 38.6-40.5 ms, profiles/r05/hyb/)
+    constexpr bool FLAGS = G <= 32;
     unsigned* ct = cnt + (size_t)t * 64;
+    auto arrive = [&](int n) {
+        if constexpr (FLAGS)
+            __hip_atomic_store((gu32*)(ct + g), (unsigned)n + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            __hip_atomic_fetch_add((gu32*)ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
     const int n_end = we;
     constexpr int m2 = N2 * N2;
     const int ev_lim = p.ev_start[t + 1];
@@ -296,8 +305,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         }
         // the output workgroup arrives at the top of the step: it has gathered step n - 1, so the row workgroups may
         // reuse that slot for step n + 1 once their poll of step n has seen this (the counter counts G per step)
-        if (ow && n < n_end && tid == 0)
-            __hip_atomic_store((gu32*)(ct + g), (unsigned)n + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (ow && n < n_end && tid == 0) arrive(n);
         // ---- column phase
         const bool fz = p.fuse && n >= 1 && !has_event(n);
         int rb;  // row g of the state the PT contracts
@@ -384,8 +392,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
                 // ---- arrive (every storing wave drained, then one lane); the wait for the group is below
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
-                if (tid == 0)
-                    __hip_atomic_store((gu32*)(ct + g), (unsigned)n + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (tid == 0) arrive(n);
             }
         }
         stamp(n, 3);
@@ -470,10 +477,15 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
                 unsigned spins = 0;
                 bool ok = true;
                 for (;;) {
-                    const unsigned v = lane < G
-                                           ? __hip_atomic_load((gu32*)(ct + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                           : want;
-                    if (__all(v >= want)) break;
+                    if constexpr (FLAGS) {
+                        const unsigned v =
+                            lane < G ? __hip_atomic_load((gu32*)(ct + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     : want;
+                        if (__all(v >= want)) break;
+                    } else {
+                        if (__hip_atomic_load((gu32*)ct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)G * want)
+                            break;
+                    }
                     __builtin_amdgcn_s_sleep(1);
                     if (++spins > p.spin_limit) { ok = false; break; }
                 }
