@@ -110,6 +110,10 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         if (tl >= p.split_xcd) return;  // an unused block (before any shared state is touched)
     }
     const bool ow = OWG && g == N2;
+    // counter form: the row workgroups get their next PT row from the gather (rowg); workgroup 0 without the output
+    // workgroup writes the outputs, so it gathers the whole state and forms its row in the column phase, as the
+    // granule form does
+    const bool rowg = !GRAN && (OWG || g != 0);
     const int t = p.traj_base + tl;
     const int wb = p.wbeg[t], we = p.wend[t];
     const long long wo = p.woff[t];
@@ -315,7 +319,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
             rb = to;
             // counter form: the gather of step n - 1 left row g of F(n) Q in PRT (pre was set): chi = 64 as the row
             // itself (each wave wrote its own k-range), else as KG partial sums
-            if (!ow && GRAN) {
+            if (!ow && !rowg) {
                 if (tid < N2) smem[OPO + tid] = pre ? frow : gld(fw_F(p, sy, wn, n, m2) + (size_t)g * N2 + tid);
                 __syncthreads();
                 if (tid < CHI) {
@@ -350,10 +354,10 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         // ---- PT row g: y = row . S(n) -> exchange buffer (parity n & 1)
         if (!ow) {
             double2 acc = c_zero();
-            if (!GRAN && fz && CHI == 64) {
+            if (rowg && fz && CHI == 64) {
 #pragma unroll
                 for (int j = 0; j < KPER; ++j) c_fma(acc, smem[PRT + kq * KPER + j], sreg[j]);
-            } else if (!GRAN && fz) {
+            } else if (rowg && fz) {
 #pragma unroll
                 for (int j = 0; j < KPER; ++j) {
                     const int k = kq * KPER + j;
@@ -411,7 +415,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         }
         if (fz) output(n, fw_W(p, sy, wn, n, N2));  // workgroup OG only (without OWG it publishes step n + 1 after this)
         pre = p.fuse && n + 1 < n_end && !has_event(n + 1);
-        if (GRAN) {
+        if (!rowg) {
             if (pre && tid < N2 && !ow) frow = gld(fw_F(p, sy, wn, n + 1, m2) + (size_t)g * N2 + tid);
         } else if (pre && !ow) {
             const double2* __restrict__ Fr = fw_F(p, sy, wn, n + 1, m2) + (size_t)g * N2;
@@ -512,7 +516,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
                 return make_double2(__hiloint2double((int)xr[i].y, (int)xr[i].x),
                                     __hiloint2double((int)xr[i].w, (int)xr[i].z));
             };
-            if (pre && !ow) {
+            if (pre && !ow && rowg) {
                 // a fused step next: only row g of F(n + 1) Q is needed, y[d] = sum_b F[g][b] Q[b][d]
                 double2 part = c_zero();
 #pragma unroll

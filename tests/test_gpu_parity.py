@@ -80,26 +80,32 @@ def test_sweep_pt(N, chi):
 
 @pytest.mark.parametrize("N", [2, 3, 4, 5, 6])
 @pytest.mark.parametrize("chi", [16, 32, 64])
-@pytest.mark.parametrize("split", ["0", "2g", "2c", "2c-noxcd"])
+@pytest.mark.parametrize("split", ["0", "2g", "2c", "2c-noxcd", "2c-noow"])
 def test_sweep_pt_split_groups(monkeypatch, N, chi, split):
-    """small batches: each trajectory over N^2 workgroups gathering its state through global memory once per
-    step (pt_split.hip), forced (2g: data-tagged granule exchange; 2c: the counter exchange, the default; both
-    with each group's workgroups dealt onto one XCD; 2c-noxcd: the plain grid) and off (0), with MTOs of every
-    kind (uneven work per group), ragged windows, several systems and a repeated slice (the slice row kept in
-    registers across steps)"""
+    """small batches: each trajectory over N^2 (+ 1) workgroups gathering its state through global memory once per
+    step (pt_split.hip), forced (2g: data-tagged granule exchange; 2c: the counter exchange with the output
+    workgroup, the default; both with each group's workgroups dealt onto one XCD; 2c-noxcd: the plain grid;
+    2c-noow: the counter exchange with workgroup 0 writing the outputs) and off (0), with MTOs of every kind (uneven
+    work per group), ragged windows, several systems and a repeated slice (the slice row kept in registers across
+    steps); the forced cases check that the plan really ran split groups"""
     monkeypatch.setenv("PQD_SPLIT", split[0])
     monkeypatch.setenv("PQD_SPLIT_GRAN", "1" if split == "2g" else "0")
     monkeypatch.setenv("PQD_SPLIT_XCD", "0" if split.endswith("noxcd") else "1")
+    monkeypatch.setenv("PQD_SPLIT_OW", "0" if split.endswith("noow") else "1")
     systems = [H.random_system(N, n_steps=30, seed=40 + k)[0] for k in range(3)]
     grid = Grid(0.0, 0.1, 30)
-    n_traj = max(1, min(7, 256 // (N * N)))
+    n_traj = max(1, min(7, 256 // (N * N + 1)))  # every group resident (N^2 + 1 workgroups with the output one)
     tr = _traj(grid.n_steps, N, n_traj, seed=N + chi)
     tr.system = np.array([k % 3 for k in range(n_traj)])
     pt = ptmod.random_pt(N, chi, D=min(N * N, 9), n_slices=9, seed=chi + N, eps=0.15)
     ops = [H.ketbra(N, 0, 0), H.ketbra(N, 1, 0), np.eye(N)]
     rho0 = H.random_rho(N)
-    cmp_lists(engine.propagate(systems, grid, rho0, ops, tr, pt=pt),
-              oracle.propagate(systems, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
+    plan = engine.Plan(systems, grid, rho0, ops, tr, pt=pt)
+    plan.execute()
+    got = plan.download()
+    if split != "0":
+        assert plan.info()[0] == "split groups" and plan.info()[2] == 0
+    cmp_lists(got, oracle.propagate(systems, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
 
 
 @pytest.mark.parametrize("N", [3, 4, 6])
