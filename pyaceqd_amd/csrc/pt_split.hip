@@ -8,11 +8,12 @@
 // column phases (M_b(n-1), MTOs, outputs, M_a(n), or the fused F(n) = M_a(n) M_b(n-1)) mix rows, so
 // every workgroup gathers the whole state (N2 x chi, 16 KiB at C3) once per step and runs them
 // redundantly — ONE exchange per step instead of a row/column transpose pair.
-// Hand-off (default): a group counter. Payload stores are 8-B sc1 atomics, every storing wave drains with
-// s_waitcnt vmcnt(0), a workgroup barrier, then ONE lane adds to the group's monotonic counter; wave 0 polls it with
-// relaxed sc1 loads, the other waves wait at a barrier, and every payload load is an sc1 load — so no fences
-// (MI355X_MICROARCH.md § visibility "Valid forms" table row 1). With the XCD-grouped grid it beat the granule form
-// below (C3 5.02 vs 5.33 us per step, profiles/r04/split/xcd/).
+// Hand-off (default): arrival words. Payload stores are 8-B sc1 atomics, the storing wave drains with
+// s_waitcnt vmcnt(0), a workgroup barrier, then ONE lane stores the workgroup's arrival word (steps published; groups
+// of more than 32 workgroups add to one shared counter instead); wave 0 polls every word of the group with one relaxed
+// sc1 load per poll, the other waves wait at a barrier, and every payload load is an sc1 load — so no fences
+// (MI355X_MICROARCH.md § visibility "Valid forms" table row 1). With the XCD-grouped grid the counter form beat the
+// granule form below (C3 5.02 vs 5.33 us per step, profiles/r04/split/xcd/).
 // Output workgroup (default in the counter form, PQD_SPLIT_OW=0 off): the group gets one more workgroup, g = N2, that
 // owns no PT row. It gathers the state like its peers, writes the outputs and trunk checkpoints, and arrives at the
 // top of each step (it has read the previous slot); without it workgroup 0 ran the output pass between its publish
@@ -308,7 +309,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
                 for (int e = tid; e < E; e += SP_NT) p.ck[(size_t)c * E + e] = smem[qo + e];
         }
         // the output workgroup arrives at the top of the step: it has gathered step n - 1, so the row workgroups may
-        // reuse that slot for step n + 1 once their poll of step n has seen this (the counter counts G per step)
+        // reuse that slot for step n + 1 once their poll of step n has seen this (its word, or its add to the counter)
         if (ow && n < n_end && tid == 0) arrive(n);
         // ---- column phase
         const bool fz = p.fuse && n >= 1 && !has_event(n);
