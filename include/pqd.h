@@ -197,6 +197,7 @@ int pqd_plan_trapz(pqd_plan* plan, int32_t n_pairs, const int32_t* k_head, const
 #define PQD_PATH_BATCHED 1  /* lock-step PT sweep, bt trajectories per workgroup */
 #define PQD_PATH_SPLIT 2    /* one trajectory over N^2 workgroups (latency path) */
 #define PQD_PATH_QUAD 3     /* two-level system: four trajectories per wave set, state in registers (pt_quad.hip) */
+#define PQD_PATH_MSPLIT 4   /* several trajectories per split group: row g of TB trajectories per workgroup (pt_msplit.hip) */
 /* the path the plan runs now, its trajectories per workgroup, how many split launches fell back, and the
  * trajectory-steps one execute propagates (trajectories of one system that share a lock-step workgroup propagate
  * their common MTO-free trunk once: PQD_BRANCH) */

@@ -160,6 +160,18 @@ struct SweepParams {
     int colbig;              // N2 > 16 column phases: one pass over k for all of a wave's tiles (1, PQD_COLBIG; 0: per tile)
 };
 
+// split groups with several trajectories per group (pt_msplit.hip)
+struct MsplitParams {
+    const int* gtraj;        // n_groups * TB trajectory ids (-1: empty slot)
+    const int* gend;         // n_groups: last step of the group (max out_end of its trajectories)
+    const int* cev_start;    // n_traj + 1: composite events of trajectory t are cev[cev_start[t] .. cev_start[t + 1])
+    const int4* cev;         // (step, MTO superoperator before or -1, after or -1, system), steps ascending per trajectory
+    double2* Fev;            // [n_cev][N2 x N2]: M_a(s) S_after S_before M_b(s - 1) (M_b(-1) = 1; zero at s = n_steps)
+    double2* Wev;            // [n_cev][n_out][N2]: ovec S_before M_b(s - 1)
+    int TB, n_groups;        // trajectories per group, groups
+    int xcd;                 // > 0: XCD-grouped grid with this many groups per XCD slot; 0: plain grid
+};
+
 // ---- free propagators through the pulse windows: M(h), F(n) = M(2n) M(2n-1) and W(n) = ovec . M(2n-1) of system sys
 // are stored only where the half steps involved lie inside the system's window [lo, hi]; outside, the propagator is
 // the idle one (the same bits the builder copied there before windows: Midle, and Fidle / Widle computed from it by
@@ -280,6 +292,13 @@ int split_blocks_per_cu(int N2, int CHI);
 hipError_t launch_split(int N2, int CHI, int n_traj, const SweepParams& p, double2* X, unsigned* cnt,
                         unsigned* err, hipStream_t s, int chunk = 0);
 bool sweep_supported(int N2, int CHI);
+// split groups carrying TB trajectories each (pt_msplit.hip)
+bool msplit_supported(int N2, int CHI, int n_out);
+int msplit_tbmax(int CHI);
+int msplit_blocks_per_cu(int N2, int CHI);
+hipError_t launch_evcomp(int N2, const SweepParams& p, const MsplitParams& q, int n_cev, int n_steps, hipStream_t s);
+hipError_t launch_msplit(int N2, int CHI, const SweepParams& p, const MsplitParams& q, double2* X, unsigned* cnt,
+                         unsigned* err, hipStream_t s);
 // the register-resident TLS sweep (pt_quad.hip): four trajectories per block, CHI/16 waves each
 bool quad_supported(int N2, int CHI);
 // ncg: 4-column groups per wave, 4 (strips of 16 columns, one wave per SIMD) or 2 (strips of 8, two waves per SIMD)

@@ -245,6 +245,14 @@ struct pqd_plan {
     int qpw = 2;         // quads per workgroup (PQD_QPW)
     int qcg = 4;         // 4-column groups per wave (PQD_QCG; auto: 2 when the quads do not fill the CUs)
     int split_chunk = 0; // split groups: trajectories per launch when the batch exceeds the device (0: one launch)
+    // split groups carrying several trajectories each (pt_msplit.hip): composite MTO operators, groups, exchange
+    bool msplit = false;
+    MsplitParams mq{};
+    int n_cev = 0;
+    DevBuf<int> ms_gtraj, ms_gend, cev_start;
+    DevBuf<int4> cev;
+    DevBuf<double2> Fev, Wev, msX;
+    DevBuf<unsigned> ms_cnt;
     DevBuf<double2> Xs;
     DevBuf<unsigned> cnt, err;
     DevBuf<double2> L0, S, T, samples, M, Midle, F, W, rho0, ovec, sop, out;
@@ -831,8 +839,13 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
         // a batch just above what the device holds runs as consecutive co-resident launches (up to 4 at N2 >= 25,
         // 2 below: a group step is 3.6x / 2.4x faster than a batched block's)
         const int fit = bpc >= 1 ? (n_cu * bpc) / split_group_size(N2) : 0;
-        const int max_launches = N2 >= 25 ? 4 : 2;
-        P->split = pt && mode != 0 && fit >= 1 && split_supported(N2, P->CHI, std::min(tr->n_traj, fit), n_cu * bpc) &&
+        // (not where multi-trajectory groups can take the batch: one launch of those beats consecutive launches)
+        const char* msa = getenv("PQD_MSPLIT");
+        const bool ms_can = !(msa && atoi(msa) == 0) && msplit_supported(N2, P->CHI, n_out) &&
+                            [] { const char* f = getenv("PQD_FUSE"); return f ? atoi(f) != 0 : true; }();
+        const int max_launches = ms_can ? 1 : (N2 >= 25 ? 4 : 2);
+        const char* ms = getenv("PQD_MSPLIT");  // 2: multi-trajectory split groups in place of these (A/B, tests)
+        P->split = pt && mode != 0 && !(ms && atoi(ms) == 2) && fit >= 1 && split_supported(N2, P->CHI, std::min(tr->n_traj, fit), n_cu * bpc) &&
                    tr->n_traj <= max_launches * fit && (mode == 2 || N2 >= 9);
         P->split_chunk = P->split && tr->n_traj > fit ? fit : 0;
     }
@@ -860,7 +873,45 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
         P->branch = (e && atoi(e) == 0) ? 0 : 1;
     }
     const bool fuse_on = !P->nopt && ns > 0 && [] { const char* f = getenv("PQD_FUSE"); return f ? atoi(f) != 0 : true; }();
-    const bool branch_on = P->branch != 0 && pt != nullptr && !P->split;
+    // batches the single-trajectory split groups do not take: split groups of TB trajectories each (pt_msplit.hip),
+    // G = N2 workgroups per group, up to 32 / N2 groups per XCD (their hand-offs in one L2). PQD_MSPLIT: 0 off, 1 auto,
+    // 2 whenever supported; PQD_MS_TB forces the trajectories per group
+    int ms_groups = 0, ms_TB = 0, ms_xcd = 0;
+    {
+        const char* e = getenv("PQD_MSPLIT");
+        int mode = e ? atoi(e) : 1;
+        // PQD_SPLIT=0 (batched kernel only) and a forced trunk pre-pass (PQD_TRUNK=1) keep the batched path
+        if (const char* sp0 = getenv("PQD_SPLIT"); sp0 && atoi(sp0) == 0) mode = 0;
+        if (const char* tk = getenv("PQD_TRUNK"); tk && atoi(tk) == 1 && mode == 1) mode = 0;
+        const int bpc = (pt && !P->split && mode != 0 && fuse_on && tr->n_traj >= 1 && msplit_supported(N2, P->CHI, n_out))
+                            ? msplit_blocks_per_cu(N2, P->CHI) : 0;
+        if (bpc >= 1) {
+            const int resident = n_cu * bpc / N2;         // groups the device holds at once
+            const int gps = 32 / N2;                       // groups per XCD slot (32 CUs per XCD on MI355X)
+            const int max_groups = std::min(resident, gps >= 1 ? 8 * gps : resident);
+            int TB = (tr->n_traj + max_groups - 1) / std::max(1, max_groups);
+            if (const char* f = getenv("PQD_MS_TB")) TB = std::max(TB, atoi(f));
+            const int n_groups = (tr->n_traj + TB - 1) / TB;
+            // auto: while a group's per-step work stays below the batched kernel's per-step time
+            // (DESIGN.md §4.10); the single-trajectory groups keep the batches they fit
+            // and while shared trunks would save little: the batched sweep starts each slot at its branch step (a
+            // G2_reuse grid saves about half of its steps there), a split group runs every trajectory from step 0
+            int64_t shared = 0, total = 0;
+            for (int t = 0; t < tr->n_traj; ++t) {
+                shared += std::max(0, std::min(jv[t], tr->out_begin[t]));
+                total += tr->out_end[t] + 1;
+            }
+            const bool want = mode == 2 || (TB <= 16 && 4 * shared <= total);
+            if (want && TB <= msplit_tbmax(P->CHI) && n_groups <= resident) {
+                P->msplit = true;
+                ms_TB = TB;
+                ms_groups = n_groups;
+                ms_xcd = (gps >= 1 && n_groups <= 8 * gps) ? (n_groups + 7) / 8 : 0;
+                if (const char* x = getenv("PQD_SPLIT_XCD"); x && atoi(x) == 0) ms_xcd = 0;
+            }
+        }
+    }
+    const bool branch_on = P->branch != 0 && pt != nullptr && !P->split && !P->msplit;
     // blocks are filled in this order and may straddle systems (each wave indexes its own system's propagators),
     // so a scan with one trajectory per system still fills every slot of a workgroup
     for (size_t k = 0; k < order.size();) {
@@ -1084,6 +1135,43 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
         HIPCHK(P->cnt.alloc((size_t)P->n_traj * 64));  // split arrival flags: two 128-B lines per group
         HIPCHK(P->err.alloc(4));
     }
+    if (P->msplit) {
+        // groups: consecutive trajectories of the block order (system, longest first), TB per group
+        std::vector<int> gt((size_t)ms_groups * ms_TB, -1), ge(ms_groups, 0);
+        for (int k = 0; k < tr->n_traj; ++k) {
+            const int gi = k / ms_TB, t = order[k];
+            gt[(size_t)gi * ms_TB + k % ms_TB] = t;
+            ge[gi] = std::max(ge[gi], tr->out_end[t]);
+        }
+        // composite MTO events: one per (trajectory, step) with MTOs, the before / after superoperators of that step
+        std::vector<int4> ce;
+        std::vector<int> cs(tr->n_traj + 1, 0);
+        for (int t = 0; t < tr->n_traj; ++t) {
+            cs[t] = (int)ce.size();
+            for (int i = ev_start[t]; i < ev_start[t + 1]; ++i) {
+                const int4 v = evs[i];
+                if (ce.size() > (size_t)cs[t] && ce.back().x == v.x) {
+                    if (v.y == 0) ce.back().y = v.z; else ce.back().z = v.z;
+                } else {
+                    ce.push_back(make_int4(v.x, v.y == 0 ? v.z : -1, v.y == 0 ? -1 : v.z, tsys[t]));
+                }
+            }
+        }
+        cs[tr->n_traj] = (int)ce.size();
+        P->n_cev = (int)ce.size();
+        if (ce.empty()) ce.push_back(make_int4(INT_MAX, -1, -1, 0));
+        HIPCHK(P->ms_gtraj.upload(gt.data(), gt.size(), s));
+        HIPCHK(P->ms_gend.upload(ge.data(), ge.size(), s));
+        HIPCHK(P->cev.upload(ce.data(), ce.size(), s));
+        HIPCHK(P->cev_start.upload(cs.data(), cs.size(), s));
+        HIPCHK(P->Fev.alloc((size_t)std::max(1, P->n_cev) * m2));
+        HIPCHK(P->Wev.alloc((size_t)std::max(1, P->n_cev) * n_out * N2));
+        HIPCHK(P->msX.alloc((size_t)ms_groups * ms_TB * 2 * N2 * P->CHI));
+        HIPCHK(P->ms_cnt.alloc((size_t)ms_groups * 64));
+        HIPCHK(P->err.alloc(4));
+        P->mq = MsplitParams{P->ms_gtraj.p, P->ms_gend.p, P->cev_start.p, P->cev.p, P->Fev.p, P->Wev.p,
+                             ms_TB, ms_groups, ms_xcd};
+    }
     HIPCHK(hipStreamSynchronize(s));
     *out = guard.release();
     return PQD_OK;
@@ -1108,6 +1196,7 @@ int pqd_plan_execute(pqd_plan* P, int32_t rebuild_free) {
     if (rebuild_free && P->n_steps > 0) {
         HIPCHK(launch_free_prop(P->N2, P->fp, s));
         if (P->sp.fuse) HIPCHK(launch_fuse_steps(P->N2, P->fu, s));
+        if (P->msplit) HIPCHK(launch_evcomp(P->N2, P->sp, P->mq, P->n_cev, P->n_steps, s));
     }
     HIPCHK(hipEventRecord(e[1], s));
     HIPCHK(launch_trunks(P, s));
@@ -1115,6 +1204,8 @@ int pqd_plan_execute(pqd_plan* P, int32_t rebuild_free) {
         HIPCHK(launch_sweep_nopt(P->N2, P->n_traj, P->sp, s));
     else if (P->split)
         HIPCHK(launch_split(P->N2, P->CHI, P->n_traj, P->sp, P->Xs.p, P->cnt.p, P->err.p, s, P->split_chunk));
+    else if (P->msplit)
+        HIPCHK(launch_msplit(P->N2, P->CHI, P->sp, P->mq, P->msX.p, P->ms_cnt.p, P->err.p, s));
     else
         HIPCHK(launch_main(P, s));
     HIPCHK(hipEventRecord(e[2], s));
@@ -1147,12 +1238,13 @@ int pqd_plan_synchronize(pqd_plan* P) {
             HIPCHK(launch_main(P, s));
         }
     }
-    if (P->split) {
+    if (P->split || P->msplit) {
         unsigned err = 0;
         HIPCHK(hipMemcpyAsync(&err, P->err.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         if (err) {
             P->split = false;
+            P->msplit = false;
             P->split_fallbacks++;
             HIPCHK(hipMemsetAsync(P->err.p, 0, sizeof(unsigned), s));
             HIPCHK(launch_main(P, s));
@@ -1266,8 +1358,10 @@ int pqd_plan_windows(const pqd_plan* P, int32_t* on) {
 int pqd_plan_info(const pqd_plan* P, int32_t* path, int32_t* bt, int32_t* split_fallbacks, int64_t* traj_steps) {
     if (!P) return fail(PQD_ERR_ARG, "plan is NULL");
     if (traj_steps) *traj_steps = P->traj_steps;
-    if (path) *path = P->nopt ? PQD_PATH_NOPT : P->split ? PQD_PATH_SPLIT : P->quad ? PQD_PATH_QUAD : PQD_PATH_BATCHED;
-    if (bt) *bt = P->BT;
+    if (path)
+        *path = P->nopt ? PQD_PATH_NOPT : P->split ? PQD_PATH_SPLIT : P->msplit ? PQD_PATH_MSPLIT
+              : P->quad ? PQD_PATH_QUAD : PQD_PATH_BATCHED;
+    if (bt) *bt = P->msplit ? P->mq.TB : P->BT;
     if (split_fallbacks) *split_fallbacks = P->split_fallbacks;
     return PQD_OK;
 }

@@ -369,7 +369,7 @@ class Plan:
         _lib.check(_lib.lib().pqd_plan_synchronize(self.handle))
 
     PATHS = {0: "no PT (one wave per trajectory)", 1: "batched lock-step sweep", 2: "split groups",
-             3: "register-resident TLS quads"}
+             3: "register-resident TLS quads", 4: "split groups, several trajectories per group"}
 
     def info(self):
         """(path name, trajectories per workgroup, split launches that fell back to the batched kernel)"""

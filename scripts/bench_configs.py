@@ -18,6 +18,9 @@ algorithmic flops (fused half steps: F = 8 (D chi^2 + chi N^4 + n_out N^2), D = 
   c4g     the same workload on a GPU-generated biexciton PT at dt = 0.1 and the reference's biexciton parameters
           (four_level_system/linear.py: t_mem 20.48 -> K = 205, a_e 3 nm, 4 K, threshold 1e-10, bond cap 128): the
           workload the drop-in produces with phonons; c4g2k: n_tau = 2,000
+  c4full  SURVEY §8d C4 literally: 256 t1 x 10,000 tau biexciton G2 sweep, chi = 64, one GPU (north star's 10x
+          target workload), auto path vs PQD_MSPLIT=0, plus the CPU port on the same trajectories
+  c4shard one rank's 32-t1 block of the same sweep split over 8 GPUs (t1 steps 96..127)
   c5dm    C5 as specified: sixls_linear + polarisation-entanglement tomography (calc_densitymatrix_reuse) over an
           e0 x bx grid (2 x {0, 1, 2, 4} points, tests/six_level_linear.py pulse pair, tend 400 ps, dt 0.1 ps, the
           class's t1 grid, chi = 64 dictionary PT), three launches for the whole grid (densitymatrix_reuse_scan)
@@ -219,6 +222,61 @@ def run_c4reuse(steps, n_scan=8, n_t1=1024, n_steps=4096, chi=64):
     return row
 
 
+def run_c4_literal(steps, n_t1=256, t1_offset=0, name="c4full", cpu=True):
+    """SURVEY §8d C4 as the north star defines it: one biexciton G2(t1, tau) sweep, n_t1 t1 points (t1 = 0.1 ps
+    steps from t1_offset) x 10,000 tau steps, chi = 64, the bench PT (bench.build_workload, one scan point).
+    c4full = the whole 256-point grid on one GPU; c4shard = one rank's 32-point block of the 8-GPU split
+    (t1_offset = 96: rank 3). Timed on the automatic path and, for comparison, with the multi-trajectory split
+    groups off (PQD_MSPLIT=0, the previous chooser); the CPU port (oracle/pqd_oracle_blk.c, OpenMP over lockstep
+    blocks of 8) on the same trajectories"""
+    import bench
+    from pyaceqd_amd import engine
+    sysd, grid, pt, rho0, ops, tr = bench.build_workload(n_t1, 10000, 64, t1_offset=t1_offset)
+    executed = int(np.sum(tr.out_end + 1))
+    useful = int(tr.n_traj * 10000)
+    row = {"config": name, "n_t1": n_t1, "t1_offset": t1_offset, "n_tau": 10000, "chi": 64, "N": 4,
+           "grid_steps": grid.n_steps, "executed_traj_steps": executed, "useful_traj_steps": useful}
+    ref = None
+    for label, env in (("auto", {}), ("no_msplit", {"PQD_MSPLIT": "0"})):
+        for k, v in env.items():
+            os.environ[k] = v
+        plan = engine.Plan(sysd, grid, rho0, ops, tr, pt=pt)
+        for k in env:
+            os.environ.pop(k)
+        plan.execute()
+        plan.synchronize()
+        plan.timing(reset=True)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            plan.execute()
+        plan.synchronize()
+        el = (time.perf_counter() - t0) / steps
+        ms_free, ms_sweep, _ = plan.timing(reset=True)
+        out = np.concatenate([r.ravel() for r in plan.download()])
+        path, bt, fb = plan.info()
+        if ref is None:
+            ref = out
+        row[label] = {"path": path, "traj_per_group_or_block": bt, "split_fallbacks": fb,
+                      "wall_ms_per_launch": el * 1e3, "sweep_ms": ms_sweep, "free_prop_ms": ms_free,
+                      "traj_steps_per_s": executed / el, "useful_traj_steps_per_s": useful / el,
+                      "us_per_grid_step": ms_sweep * 1e3 / (grid.n_steps + 1),
+                      "max_rel_diff_vs_auto": float(np.max(np.abs(out - ref)) / np.max(np.abs(ref)))}
+    if cpu:
+        info = bench.host_cpu()
+        threads = bench.cpu_threads(info)
+        from oracle import oracle
+        t0 = time.perf_counter()
+        cres = oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt, nthreads=threads, blocked=bench.CPU_BLOCK)
+        cel = time.perf_counter() - t0
+        cout = np.concatenate([r.ravel() for r in cres])
+        row["cpu_port"] = {"wall_s": cel, "threads": threads, "blocks_of": bench.CPU_BLOCK,
+                           "busy_threads": min(threads, (tr.n_traj + bench.CPU_BLOCK - 1) // bench.CPU_BLOCK),
+                           "traj_steps_per_s": executed / cel,
+                           "max_rel_diff_vs_gpu": float(np.max(np.abs(cout - ref)) / np.max(np.abs(ref)))}
+        row["gpu_vs_cpu_wall"] = cel / (row["auto"]["wall_ms_per_launch"] * 1e-3)
+    return row
+
+
 def run_c5dm(steps, n_e0=2, bxs=(0.0, 1.0, 2.0, 4.0), tend=400.0):
     import tempfile
     from pyaceqd_amd import opgrammar, pt as ptmod
@@ -261,7 +319,9 @@ def main():
     args = ap.parse_args()
     for name in args.configs.split(","):
         # c5dm32: one rank's share of SURVEY §8d C5 (256 points = 64 e0 x 4 bx over 8 GPUs): 8 e0 x 4 bx
-        special = {"c5dm": run_c5dm, "c4reuse": run_c4reuse, "c5dm32": lambda st: run_c5dm(st, n_e0=8)}
+        special = {"c5dm": run_c5dm, "c4reuse": run_c4reuse, "c5dm32": lambda st: run_c5dm(st, n_e0=8),
+                   "c4full": run_c4_literal,
+                   "c4shard": lambda st: run_c4_literal(st, n_t1=32, t1_offset=96, name="c4shard")}
         print(json.dumps(special[name](args.steps) if name in special else run(name, args.steps)), flush=True)
 
 
