@@ -104,6 +104,9 @@ typedef struct {
 
 int32_t pqd_version(void);
 const char* pqd_last_error(void);
+/* HIP version libpqd was built against (HIP_VERSION) and the one its loaded runtime reports (hipRuntimeGetVersion);
+ * the Python loader warns when their major.minor differ (the process may have loaded another runtime first) */
+int pqd_hip_versions(int32_t* build, int32_t* runtime);
 
 int pqd_ctx_create(int32_t device, pqd_ctx** out);
 void pqd_ctx_destroy(pqd_ctx* ctx);

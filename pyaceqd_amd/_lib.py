@@ -66,6 +66,7 @@ _lock = threading.RLock()
 _SIGS = {
     "pqd_version": ([], C.c_int32),
     "pqd_last_error": ([], C.c_char_p),
+    "pqd_hip_versions": ([P_I32, P_I32], C.c_int),
     "pqd_ctx_create": ([C.c_int32, C.POINTER(C.c_void_p)], C.c_int),
     "pqd_ctx_destroy": ([C.c_void_p], None),
     "pqd_ctx_synchronize": ([C.c_void_p], C.c_int),
@@ -164,7 +165,29 @@ def lib():
                     f.argtypes = args
                     f.restype = res
                 _lib = L
+                _check_runtime(L)
     return _lib
+
+
+RUNTIME_VERSIONS = None  # (HIP version libpqd was built against, the loaded runtime's), HIP_VERSION encoding
+
+
+def _check_runtime(L):
+    """with torch imported first, libpqd binds to torch's bundled HIP runtime. The versions are kept in
+    RUNTIME_VERSIONS; a different MAJOR version warns (this image pairs ROCm 7.2 with torch's 7.0 runtime, a minor
+    difference every GPU test and bench run has used; HIP_VERSION = major 1e7 + minor 1e5 + patch)"""
+    global RUNTIME_VERSIONS
+    if not hasattr(L, "pqd_hip_versions"):
+        return
+    b, r = C.c_int32(), C.c_int32()
+    if L.pqd_hip_versions(C.byref(b), C.byref(r)) != 0:
+        return
+    RUNTIME_VERSIONS = (b.value, r.value)
+    if b.value // 10000000 != r.value // 10000000:
+        import warnings
+        warnings.warn(f"libpqd was built against HIP {b.value // 10000000}.{b.value // 100000 % 100} but the process "
+                      f"runs HIP runtime {r.value // 10000000}.{r.value // 100000 % 100} (loaded first, e.g. by torch); "
+                      f"PQD_TORCH_FIRST=0 keeps libpqd's own runtime", RuntimeWarning, stacklevel=3)
 
 
 def check(rc):

@@ -345,6 +345,14 @@ extern "C" {
 
 int32_t pqd_version(void) { return 1; }
 const char* pqd_last_error(void) { return g_err.c_str(); }
+int pqd_hip_versions(int32_t* build, int32_t* runtime) {
+    if (!build || !runtime) return fail(PQD_ERR_ARG, "NULL argument");
+    *build = HIP_VERSION;
+    int v = 0;
+    if (hipRuntimeGetVersion(&v) != hipSuccess) return fail(PQD_ERR_HIP, "hipRuntimeGetVersion failed");
+    *runtime = v;
+    return PQD_OK;
+}
 
 int pqd_ctx_create(int32_t device, pqd_ctx** out) {
     if (!out) return fail(PQD_ERR_ARG, "out is NULL");
@@ -874,7 +882,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     }
     const bool fuse_on = !P->nopt && ns > 0 && [] { const char* f = getenv("PQD_FUSE"); return f ? atoi(f) != 0 : true; }();
     // batches the single-trajectory split groups do not take: split groups of TB trajectories each (pt_msplit.hip),
-    // G = N2 workgroups per group, up to 32 / N2 groups per XCD (their hand-offs in one L2). PQD_MSPLIT: 0 off, 1 auto,
+    // G = N2 / 2 workgroups per group (N2 = 9: 9), up to 32 / G groups per XCD (their hand-offs in one L2). PQD_MSPLIT: 0 off, 1 auto,
     // 2 whenever supported; PQD_MS_TB forces the trajectories per group
     int ms_groups = 0, ms_TB = 0, ms_xcd = 0;
     {
@@ -886,8 +894,9 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
         const int bpc = (pt && !P->split && mode != 0 && fuse_on && tr->n_traj >= 1 && msplit_supported(N2, P->CHI, n_out))
                             ? msplit_blocks_per_cu(N2, P->CHI) : 0;
         if (bpc >= 1) {
-            const int resident = n_cu * bpc / N2;         // groups the device holds at once
-            const int gps = 32 / N2;                       // groups per XCD slot (32 CUs per XCD on MI355X)
+            const int G = msplit_group_size(N2);
+            const int resident = n_cu * bpc / G;          // groups the device holds at once
+            const int gps = 32 / G;                        // groups per XCD slot (32 CUs per XCD on MI355X)
             const int max_groups = std::min(resident, gps >= 1 ? 8 * gps : resident);
             int TB = (tr->n_traj + max_groups - 1) / std::max(1, max_groups);
             if (const char* f = getenv("PQD_MS_TB")) TB = std::max(TB, atoi(f));
@@ -901,8 +910,10 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
                 shared += std::max(0, std::min(jv[t], tr->out_begin[t]));
                 total += tr->out_end[t] + 1;
             }
-            const bool want = mode == 2 || (TB <= 16 && 4 * shared <= total);
-            if (want && TB <= msplit_tbmax(P->CHI) && n_groups <= resident) {
+            // (measured, profiles/r06/: 32 trajectories TB = 1 33 ms vs 124 ms batched; 256 trajectories TB = 8 114 vs
+            // 124 ms; past TB = 8 the per-step gather of TB states per workgroup is not measured to win)
+            const bool want = mode == 2 || (TB <= 8 && 4 * shared <= total);
+            if (want && TB <= msplit_tbmax(N2, P->CHI) && n_groups <= resident) {
                 P->msplit = true;
                 ms_TB = TB;
                 ms_groups = n_groups;

@@ -1,29 +1,29 @@
-// pt_msplit.hip — split groups that carry several trajectories: a group of G = N2 workgroups propagates TB
-// trajectories at once, workgroup g owning PT row alpha = g of every one of them.
+// pt_msplit.hip — split groups that carry several trajectories: a group of G = ceil(N2 / R) workgroups propagates
+// TB trajectories at once, workgroup g owning PT rows alpha = R g + h (h < R) of every one of them.
 //
 // Why: the single-trajectory split path (pt_split.hip) fits n_cu / (N2 + 1)
 // groups, 15 at N2 = 16, so the 32-t1 rank shard of the C4 sweep and the whole 256-t1 sweep fell to the batched
-// kernel: 8 or 64 workgroups, each streaming the whole 1 MiB slice set per step through its CU (≈12.8 µs per
-// step). Here every CU streams only its slice row (64 KiB at chi = 64, held in registers while the schedule repeats
-// it) and ONE slice read feeds TB trajectories, so 32 trajectories run as 16 groups of 2 on all 256 CUs and 256
-// trajectories as 16 groups of 16.
+// kernel: 8 or 64 workgroups, each streaming the whole 1 MiB slice set per step through its CU (≈12.3 µs per
+// step). Here every CU holds only its R slice rows (R x 64 KiB at chi = 64, in registers while the schedule repeats
+// them), ONE slice read feeds TB trajectories, and 32 trajectories run as 32 groups of one on all 256 CUs.
 //
-// Per step n, row workgroup g of a group:
-//   PT(n)     y_b = r_b . S_g(n) for every active trajectory b, r_b = row g of F_b(n) Q_b (from the gather of step
-//             n - 1): thread (kq, d) holds S_g[kq KPER + j][d] (j < KPER) in registers, the KG partial sums meet in LDS
+// A workgroup is R "halves" of HT = 4 CHI threads; half h owns row alpha_h = R g + h. Per step n:
+//   PT(n)     half h: y_b = r_b^h . S_alpha_h(n) for every active trajectory b, r_b^h = row alpha_h of F_b(n) Q_b
+//             (from the gather of step n - 1): thread (kq, d) holds S[kq KPER + j][d] (j < KPER) in registers, the 4
+//             k-group partial sums meet in LDS
 //   publish   y_b -> exchange slot n & 1 of trajectory b (8-B sc1 relaxed atomic stores), every storing wave drains
 //             (s_waitcnt vmcnt(0)), a barrier, then ONE lane stores the workgroup's arrival word (= n + 1)
-//   prefetch  F_b(n + 1) row g, the output rows W_b(n + 1) of the trajectories this workgroup writes, the closure
-//             column, then the next slice row when the schedule changes it (issued last: the LDS staging of the small
-//             operands waits only for their own loads)
+//   operands  F_b(n + 1) rows and the output rows W_b(n + 1) were loaded into registers during step n - 1: they go to
+//             LDS now and the loads of step n + 2's are issued (an operand load never sits between a publish and a
+//             poll); then the next slice rows when the schedule changes them
 //   poll      wave 0 reads the G arrival words of the group (one relaxed sc1 load per poll), the others wait at a barrier
-//   gather    every element of every active state, 16-B sc1 buffer loads of 4 trajectories at a time in flight:
-//             thread (kq, c, rg) takes column kq KPER + c of rows rg + 4 i, contracts them with F_b(n + 1)[g][.] and
-//             sums the 4 row groups by DPP (quad_perm): r_b for PT(n + 1) lands in the k-range the thread's own
-//             k-group contracts (chi <= 64: one wave, no barrier)
-//   outputs   trajectory b's outputs are written by workgroup b mod N2 from the state it gathers anyway: <O_k> at
-//             step n + 1 = sum W_b(n + 1)[k][beta] Q_b[beta][d] c[d], one wave sum each, the KG wave partials added
-//             after the next PT barrier — no output workgroup, so two groups of 16 fit one XCD's 32 CUs
+//   gather    half h takes the trajectories b = h, h + R, ...: every element of each state by 16-B sc1 buffer loads,
+//             up to 4 trajectories' loads in flight per thread; thread (kq, c, rg) takes column kq KPER + c of rows
+//             rg + 4 i and contracts them with F_b(n + 1)[alpha][.] for all R rows of the workgroup (each element is
+//             loaded once per workgroup), the 4 row groups summed by DPP (quad_perm); one barrier, then PT(n + 1)
+//   outputs   trajectory b's outputs are written by workgroup b mod G (the half that gathers b) from the state it
+//             loads anyway: <O_k>(n + 1) = sum W_b(n + 1)[k][beta] Q_b[beta][d] c[d], one wave sum each, the wave
+//             partials added after the next PT barrier — no output workgroup
 // MTOs: every trajectory-step with an MTO uses a composite operator, F'(n) = M_a(n) S_after S_before M_b(n - 1) and
 // W'(n) = ovec S_before M_b(n - 1) (M_b(-1) = 1), built per event on the device after the free propagators
 // (evcomp_kernel), so each step of each trajectory is one row operator and one set of output rows (the batched
@@ -41,6 +41,11 @@ typedef unsigned int __attribute__((address_space(1))) mu32;
 typedef unsigned int v4u32m __attribute__((ext_vector_type(4)));
 
 constexpr int MS_LDS_FORCE = 96 * 1024;  // dynamic LDS request: one workgroup per CU
+constexpr int MS_CEV_MAX = 512;          // composite events per group held in LDS (msplit_cev_max)
+template <int V>
+struct MsIC {  // compile-time int tag (the gather's chunk variants)
+    static constexpr int value = V;
+};
 
 __device__ __forceinline__ void ms_st_sc1(double2* p, double2 v) {
     __hip_atomic_store((mu64*)&p->x, (unsigned long long)__double_as_longlong(v.x), __ATOMIC_RELAXED,
@@ -61,65 +66,85 @@ __device__ __forceinline__ double2 ms_wave_sum(double2 v) {
     return make_double2(xor_add<32>(v.x), xor_add<32>(v.y));
 }
 
-template <int N2, int CHI>
+template <int N2, int CHI, int R>
 struct MsLayout {
-    static constexpr int KG = 4;                    // k-groups of the row contraction
-    static constexpr int KPER = CHI / KG;           // slice rows per thread: 8 / 16 / 32 (chi = 32 / 64 / 128)
-    static constexpr int NT = KG * CHI;             // threads: 128 / 256 / 512
-    static constexpr int NW = NT / 64;              // waves
+    static constexpr int KG = 4;                    // k-groups of a row contraction
+    static constexpr int KPER = CHI / KG;           // slice rows per thread: 8 / 16 (chi = 32 / 64)
+    static constexpr int HT = KG * CHI;             // threads per half (one PT row): 128 / 256
+    static constexpr int NT = R * HT;               // threads per workgroup
+    static constexpr int NW = NT / 64, NWH = HT / 64;
+    static constexpr int G = (N2 + R - 1) / R;      // workgroups per group
     static constexpr int RG = 4;                    // gather row groups: lanes 4 c + rg of a k-group
     static constexpr int EPT = (N2 + RG - 1) / RG;  // state rows per thread and trajectory in the gather
-    static constexpr int GCH = CHI == 128 ? 1 : (EPT <= 4 ? 4 : 2);  // trajectories whose gather loads are in flight together
-    static constexpr int TBMAX = CHI == 128 ? 16 : 32;
-    static constexpr int TBC = CHI == 128 ? 4 : (CHI == 64 ? 16 : 32);  // trajectories per PT pass (LDS partials)
+    static constexpr int GCH = R >= 4 ? 2 : (EPT <= 4 ? 4 : 1);  // trajectories per half with gather loads in flight
+    static constexpr int PRB = R >= 4 ? 4 : KPER;  // row values in flight in the PT (R = 4: 128 registers per thread)
+    static constexpr int TBMAX = R == 1 ? 32 : (R == 2 ? 16 : 8);
+    static constexpr int TBC = R >= 4 ? 4 : 8;      // trajectories per PT pass (LDS partials)
     static constexpr int OMAX = 8;                  // outputs per trajectory
-    static constexpr int TMINE = (TBMAX + N2 - 1) / N2;  // trajectories whose outputs one workgroup writes
-    static constexpr int FPT = (TBMAX * N2 + NT - 1) / NT;          // F-row entries per thread
+    static constexpr int TMINE = (TBMAX + G - 1) / G;  // trajectories whose outputs one workgroup writes
+    static constexpr int FPT = (R * TBMAX * N2 + NT - 1) / NT;      // F-row entries per thread
     static constexpr int WPT = (TMINE * OMAX * N2 + NT - 1) / NT;   // output-row entries per thread
-    static constexpr int PRO = 0;                      // r_b rows [TBMAX][CHI]
-    static constexpr int REDO = PRO + TBMAX * CHI;     // PT partials [TBC][NT]
-    static constexpr int FRO = REDO + TBC * NT;        // F_b(n + 1) row g [TBMAX][N2]
-    static constexpr int WLO = FRO + TBMAX * N2;       // output rows [TMINE][OMAX][N2]
-    static constexpr int OPO = WLO + TMINE * OMAX * N2;  // output wave partials [TMINE][OMAX][NW]
-    static constexpr int END = OPO + TMINE * OMAX * NW;
+    static constexpr int PRO = 0;                        // r_b rows [R][TBMAX][CHI]
+    static constexpr int REDO = PRO + R * TBMAX * CHI;   // PT partials [R][TBC][HT]
+    static constexpr int FRO = REDO + R * TBC * HT;      // F_b(n + 1) rows of the workgroup [R][TBMAX][N2]
+    static constexpr int WLO = FRO + R * TBMAX * N2;     // output rows [TMINE][OMAX][N2]
+    static constexpr int CLO = WLO + TMINE * OMAX * N2;  // closure vector of the outputs the gather writes [CHI]
+    static constexpr int OPO = CLO + CHI;                // output columns (W row x state, times the closure) [TMINE][OMAX][CHI]
+    static constexpr int DUMMY = OPO + TMINE * OMAX * CHI;  // write target of out-of-range operand entries
+    static constexpr int END = DUMMY + 1;
     static constexpr int LDS = END * 16 > MS_LDS_FORCE ? END * 16 : MS_LDS_FORCE;
 };
 
-template <int N2, int CHI>
-__global__ __launch_bounds__(4 * CHI) void pt_msplit_kernel(SweepParams p, MsplitParams q,
-                                                                           double2* __restrict__ X,
-                                                                           unsigned* __restrict__ cnt,
-                                                                           unsigned* __restrict__ err) {
-    using L = MsLayout<N2, CHI>;
-    constexpr int NT = L::NT, KG = L::KG, KPER = L::KPER, RG = L::RG, EPT = L::EPT, NW = L::NW;
-    constexpr int E = N2 * CHI, m2 = N2 * N2;
+// diagnostics (PQD_ABLATE bit 64, scripts/msplit_stamps.py): s_memtime at the phase boundaries of steps 1000..1015 in
+// workgroups 0 and 1 of group 0 (thread 0): [wg][step][phase 0..7]
+__device__ unsigned long long g_ms_stamps[2 * 16 * 8];
+
+template <int N2, int CHI, int R, bool STAMP = false>
+__global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, MsplitParams q,
+                                                                 double2* __restrict__ X, unsigned* __restrict__ cnt,
+                                                                 unsigned* __restrict__ err) {
+    using L = MsLayout<N2, CHI, R>;
+    constexpr int NT = L::NT, HT = L::HT, KG = L::KG, KPER = L::KPER, RG = L::RG, EPT = L::EPT, NW = L::NW;
+    constexpr int G = L::G, E = N2 * CHI, m2 = N2 * N2, TBM = L::TBMAX;
     static_assert(L::LDS <= 160 * 1024, "LDS budget");
     static_assert(KPER * KG == CHI && CHI / RG == KPER, "gather columns = the k-group's slice rows");
     extern __shared__ __attribute__((aligned(16))) double2 smem[];
     __shared__ int s_abort;
-    __shared__ int s_t[L::TBMAX], s_wb[L::TBMAX], s_we[L::TBMAX], s_sy[L::TBMAX];
-    __shared__ int s_evs[L::TBMAX], s_evi[L::TBMAX], s_eve[L::TBMAX];
-    __shared__ long long s_wo[L::TBMAX];
+    __shared__ int s_wb[TBM], s_we[TBM], s_sy[TBM];
+    __shared__ int s_evs[TBM], s_evi[TBM], s_eve[TBM];  // first composite step, its index, the end of the list
+    __shared__ int s_cvo[TBM];                          // where trajectory slot b's composite steps start in s_cev
+    __shared__ int s_cev[MS_CEV_MAX];                   // the group's composite steps (host: at most MS_CEV_MAX)
+    __shared__ long long s_wo[TBM];
 
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int h = tid / HT, ht = tid - h * HT;  // half, thread within the half
     int grp, g;
     if (q.xcd > 0) {
         // XCD-grouped grid: block b sits in XCD slot b % 8 under the observed round-robin dealing; slot xs holds the
         // groups xs, xs + 8, ... so each group's hand-offs stay in one L2 (speed only, as in pt_split.hip)
         const int xs = blockIdx.x & 7, loc = blockIdx.x >> 3;
-        grp = xs + 8 * (loc / N2);
-        g = loc - (loc / N2) * N2;
+        grp = xs + 8 * (loc / G);
+        g = loc - (loc / G) * G;
     } else {
-        grp = blockIdx.x / N2;
-        g = blockIdx.x - grp * N2;
+        grp = blockIdx.x / G;
+        g = blockIdx.x - grp * G;
     }
     if (grp >= q.n_groups) return;  // an unused block (before any shared state is touched)
     const int TB = q.TB, n_out = p.n_out;
     const int n_end = q.gend[grp];
+    // phase stamps: 0 top, 1 PT partials (barrier), 2 published + arrived, 3 operands staged, 4 peers arrived (poll +
+    // barrier), 5 gather loads and operand loads issued, 6 gather done, 7 end barrier
+    auto stamp = [&](int n, int k) {
+        if constexpr (STAMP) {
+            if (grp == 0 && g < 2 && threadIdx.x == 0 && n >= 1000 && n < 1016)
+                g_ms_stamps[(g * 16 + (n - 1000)) * 8 + k] = __builtin_amdgcn_s_memtime();
+        }
+    };
+    const int alpha = R * g + h;          // this half's PT row
+    const bool live = alpha < N2;         // (the last workgroup of a group may own fewer than R rows)
     if (tid == 0) s_abort = 0;
     if (tid < TB) {
         const int t = q.gtraj[grp * TB + tid];
-        s_t[tid] = t;
         s_wb[tid] = t >= 0 ? p.wbeg[t] : INT_MAX;
         s_we[tid] = t >= 0 ? p.wend[t] : -1;
         s_sy[tid] = t >= 0 ? p.traj_sys[t] : 0;
@@ -129,18 +154,19 @@ __global__ __launch_bounds__(4 * CHI) void pt_msplit_kernel(SweepParams p, Mspli
         s_eve[tid] = i1;
         s_evs[tid] = i0 < i1 ? q.cev[i0].x : INT_MAX;
     }
-    // exchange of this group: slot (b, parity) of trajectory slot b at X + ((grp TB + b) 2 + parity) E
+    // exchange of this group: slot (b, parity) at Xg + (2 b + parity) E
     double2* __restrict__ Xg = X + (size_t)grp * TB * 2 * E;
     const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(Xg, 0, TB * 2 * E * 16, 0x00020000);
     unsigned* ct = cnt + (size_t)grp * 64;
 
-    // thread roles: PT (kq, j): slice rows kq KPER + jj, column j; gather (kq, c = j / RG, rg = j % RG): column
-    // kcol = kq KPER + c of rows rg + RG i
-    const int kq = tid / CHI, j = tid - kq * CHI, cgi = j / RG, rg = j - cgi * RG;
+    // thread roles in its half: PT (kq, j): slice rows kq KPER + jj, column j; gather (kq, c = j / RG, rg = j % RG):
+    // column kcol = kq KPER + c of rows rg + RG i
+    const int kq = ht / CHI, j = ht - kq * CHI, cgi = j / RG, rg = j - cgi * RG;
     const int kcol = kq * KPER + cgi;
-    const int grow = p.gmap[g];
+    const int grow = live ? p.gmap[alpha] : 0;
     double2 sreg[KPER];
     auto fetch_slice = [&](int si) {
+        if (!live) return;
         const double2* __restrict__ S = p.Q + ((size_t)si * p.D + grow) * CHI * CHI;
 #pragma unroll
         for (int jj = 0; jj < KPER; ++jj) sreg[jj] = ms_gld(S + (size_t)(kq * KPER + jj) * CHI + j);
@@ -150,152 +176,251 @@ __global__ __launch_bounds__(4 * CHI) void pt_msplit_kernel(SweepParams p, Mspli
         const int i = 64 * ch + lane;
         return i < n_end ? *(const __attribute__((address_space(1))) int*)(p.sched + i) : -1;
     };
-    int sch_cur = sched_chunk(0), sch_nxt = sched_chunk(1);
-    int cur_slice = n_end > 0 ? __builtin_amdgcn_readlane(sch_cur, 0) : -1;
+    int sch_reg = sched_chunk(0);  // the chunk of sched[m] for the coming step's m = n + 1, loaded a step ahead
+    int cur_slice = n_end > 0 ? __builtin_amdgcn_readlane(sch_reg, 0) : -1;
     if (n_end > 0) fetch_slice(cur_slice);
     __syncthreads();
 
-    // ---- step 0: r_b = row g of F_b(0) Q_b(0), Q_b(0) = rho0 (x) bond0, F_b(0) = M_a(0) or the composite at step 0;
-    // outputs at step 0 of this workgroup's trajectories directly
-    for (int e = tid; e < TB * CHI; e += NT) {
-        const int b = e / CHI, k = e - b * CHI;
-        if (s_we[b] <= 0) continue;
-        const int sy = s_sy[b];
+    // composite event index of trajectory b at step 0 (-1: none); step 0 only — the loop keeps per-entry cursors
+    auto comp0 = [&](int b) { return s_evs[b] == 0 ? s_evi[b] : -1; };
+
+    // ---- step 0: r_b^h = row alpha_h of F_b(0) Q_b(0), Q_b(0) = rho0 (x) bond0, F_b(0) = M_a(0) or the composite at
+    // step 0; outputs at step 0 of this workgroup's trajectories directly
+    for (int e = tid; e < R * TB * CHI; e += NT) {
+        const int r = e / (TB * CHI), b = (e / CHI) % TB, k = e % CHI, a = R * g + r;
+        if (s_we[b] <= 0 || a >= N2) continue;
+        const int sy = s_sy[b], ci = comp0(b);
         const double2* __restrict__ Fr =
-            (s_evs[b] == 0 ? q.Fev + (size_t)s_evi[b] * m2 : fw_M(p, sy, fw_win(p, sy), 0, m2)) + (size_t)g * N2;
+            (ci >= 0 ? q.Fev + (size_t)ci * m2 : fw_M(p, sy, fw_win(p, sy), 0, m2)) + (size_t)a * N2;
         double2 acc = c_zero();
         for (int be = 0; be < N2; ++be) c_fma(acc, ms_gld(Fr + be), ms_gld(p.rho0 + be));
-        smem[L::PRO + b * CHI + k] = c_mul(acc, ms_gld(p.bond0 + k));
+        smem[L::PRO + (r * TBM + b) * CHI + k] = c_mul(acc, ms_gld(p.bond0 + k));
     }
     for (int e = tid; e < TB * n_out; e += NT) {
         const int b = e / n_out, k = e - b * n_out;
-        if (b % N2 != g || s_wb[b] != 0 || s_we[b] < 0) continue;
-        const double2* __restrict__ W0 =
-            s_evs[b] == 0 ? q.Wev + (size_t)s_evi[b] * n_out * N2 : p.ovec;
+        if (b % G != g || s_wb[b] != 0 || s_we[b] < 0) continue;
+        const int ci = comp0(b);
+        const double2* __restrict__ W0 = ci >= 0 ? q.Wev + (size_t)ci * n_out * N2 : p.ovec;
         double2 r = c_zero(), bc = c_zero();
         for (int be = 0; be < N2; ++be) c_fma(r, ms_gld(W0 + (size_t)k * N2 + be), ms_gld(p.rho0 + be));
         for (int d = 0; d < CHI; ++d) c_fma(bc, ms_gld(p.bond0 + d), ms_gld(p.closure0 + d));
         p.out[s_wo[b] + k] = c_mul(r, bc);
     }
+
+    // the group's composite steps into LDS, so an operand entry's cursor advances with LDS reads: a global load there
+    // would leave a register pending across the step loop, and the waits for it (in-order vmcnt) would hold the gather
     __syncthreads();
-    if (tid < TB && s_evs[tid] == 0) {
-        const int i = ++s_evi[tid];
-        s_evs[tid] = i < s_eve[tid] ? q.cev[i].x : INT_MAX;
+    if (tid == 0) {
+        int o = 0;
+        for (int b = 0; b < TB; ++b) { s_cvo[b] = o; o += s_eve[b] - s_evi[b]; }
     }
     __syncthreads();
+    for (int b = 0; b < TB; ++b)
+        for (int i = tid; i < s_eve[b] - s_evi[b]; i += NT) s_cev[s_cvo[b] + i] = q.cev[s_evi[b] + i].x;
+    __syncthreads();
 
-    const int tmine = (TB - g + N2 - 1) / N2;  // trajectories b = g + N2 mb whose outputs this workgroup writes
-    // the wave partials of the outputs at step n gathered during step n - 1, summed and stored
-    auto flush = [&](int n) {
-        for (int e = tid; e < tmine * n_out; e += NT) {
-            const int mb = e / n_out, k = e - mb * n_out, b = g + N2 * mb;
-            if (n < s_wb[b] || n > s_we[b]) continue;
-            double2 o = smem[L::OPO + (mb * L::OMAX + k) * NW];
+    const int tmine = (TB - g + G - 1) / G;  // trajectories b = g + G mb whose outputs this workgroup writes
+    const int wrow = n_out * N2;
+    // per-step activity as wave-uniform bit masks (bit b = trajectory slot b): lane b < TB holds its window
+    const int my_wb = lane < TB ? s_wb[lane] : INT_MAX, my_we = lane < TB ? s_we[lane] : -1;
+    auto mask = [](bool c) { return (unsigned long long)__ballot(c); };
+
+    // operand entries, fixed for the launch: F entry i = (row a, slot b, column be) of F_b(m)[a][be]; W entry i =
+    // (output slot mb, element rr) of W_b(m). Each keeps its trajectory's system base, window and a composite cursor
+    // (next composite step / index / end) in registers, so the per-step loads need no LDS reads or table lookups. The
+    // split paths run without pulse windows (pqd_host.cpp: windows only for the quad and no-PT kernels), so F(m) and
+    // W(m) are the stored operators.
+    // cursors: ci = position in s_cev, ce = its end, cg = global composite index - position, cs = s_cev[ci] or INT_MAX
+    const double2* fbase[L::FPT];
+    int f_row[L::FPT], f_we[L::FPT], f_cs[L::FPT], f_ci[L::FPT], f_ce[L::FPT], f_cg[L::FPT];
+    const double2* wbase[L::WPT];
+    int w_rr[L::WPT], w_wb[L::WPT], w_we[L::WPT], w_cs[L::WPT], w_ci[L::WPT], w_ce[L::WPT], w_cg[L::WPT];
+    auto first_comp = [&](int b, int from, int& cs, int& ci, int& ce, int& cg) {
+        int i = s_cvo[b];
+        ce = i + s_eve[b] - s_evi[b];
+        cg = s_evi[b] - i;
+        while (i < ce && s_cev[i] < from) ++i;
+        ci = i;
+        cs = i < ce ? s_cev[i] : INT_MAX;
+    };
 #pragma unroll
-            for (int w = 1; w < NW; ++w) o = c_add(o, smem[L::OPO + (mb * L::OMAX + k) * NW + w]);
-            p.out[s_wo[b] + (long long)(n - s_wb[b]) * n_out + k] = o;
+    for (int i = 0; i < L::FPT; ++i) {
+        const int e = tid + NT * i;
+        const bool in = e < R * TB * N2;
+        const int r = in ? e / (TB * N2) : 0, b = in ? (e / N2) % TB : 0, be = e % N2, a = R * g + r;
+        f_row[i] = a * N2 + be;
+        fbase[i] = p.F + (size_t)s_sy[b] * p.f_stride + f_row[i];
+        f_we[i] = (in && a < N2) ? s_we[b] : -1;
+        first_comp(b, 1, f_cs[i], f_ci[i], f_ce[i], f_cg[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < L::WPT; ++i) {
+        const int e = tid + NT * i;
+        const int mb = e / wrow, rr = e - mb * wrow;
+        const bool in = mb < tmine;
+        const int b = in ? g + G * mb : 0;
+        w_rr[i] = rr;
+        wbase[i] = p.W + (size_t)s_sy[b] * p.w_stride + rr;
+        w_wb[i] = in ? s_wb[b] : INT_MAX;
+        w_we[i] = in ? s_we[b] : -1;
+        first_comp(b, 1, w_cs[i], w_ci[i], w_ce[i], w_cg[i]);
+    }
+    // operands of step m into registers (staged into LDS one step later). Every lane issues the same number of loads
+    // (entries it does not need read rho0[0]), so the gather's waits can leave them in flight.
+    double2 fpre[L::FPT], wpre[L::WPT];
+    double2 clv = c_zero();  // the closure vector of the outputs at step m + 1 (the slice PT(m) uses), with step m's operands
+    auto load_ops = [&](int m) {
+#pragma unroll
+        for (int i = 0; i < L::FPT; ++i) {
+            const double2* src = p.rho0;
+            if (m < f_we[i]) {
+                src = fbase[i] + (size_t)m * m2;
+                if (m >= f_cs[i]) {  // rare: a composite at m (cursor moved past composites before m)
+                    while (f_cs[i] < m) { ++f_ci[i]; f_cs[i] = f_ci[i] < f_ce[i] ? s_cev[f_ci[i]] : INT_MAX; }
+                    if (f_cs[i] == m) {
+                        src = q.Fev + (size_t)(f_ci[i] + f_cg[i]) * m2 + f_row[i];
+                        ++f_ci[i];
+                        f_cs[i] = f_ci[i] < f_ce[i] ? s_cev[f_ci[i]] : INT_MAX;
+                    }
+                }
+            }
+            fpre[i] = ms_gld(src);
+        }
+#pragma unroll
+        for (int i = 0; i < L::WPT; ++i) {
+            const double2* src = p.rho0;
+            if (m >= w_wb[i] && m <= w_we[i]) {
+                src = wbase[i] + (size_t)m * wrow;
+                if (m >= w_cs[i]) {
+                    while (w_cs[i] < m) { ++w_ci[i]; w_cs[i] = w_ci[i] < w_ce[i] ? s_cev[w_ci[i]] : INT_MAX; }
+                    if (w_cs[i] == m) {
+                        src = q.Wev + (size_t)(w_ci[i] + w_cg[i]) * wrow + w_rr[i];
+                        ++w_ci[i];
+                        w_cs[i] = w_ci[i] < w_ce[i] ? s_cev[w_ci[i]] : INT_MAX;
+                    }
+                }
+            }
+            wpre[i] = ms_gld(src);
         }
     };
-
-    double2 fpre[L::FPT], wpre[L::WPT];
-#pragma unroll
-    for (int i = 0; i < L::FPT; ++i) fpre[i] = c_zero();
-#pragma unroll
-    for (int i = 0; i < L::WPT; ++i) wpre[i] = c_zero();
-    for (int n = 0;; ++n) {
-        if (n >= n_end) {
-            __syncthreads();
-            if (n >= 1) flush(n);
-            break;
-        }
-        // ---- PT(n) for the trajectories that continue past n, TBC at a time (LDS partials)
-        for (int b0 = 0; b0 < TB; b0 += L::TBC) {
-            const int nb = TB - b0 < L::TBC ? TB - b0 : L::TBC;
-            for (int bb = 0; bb < nb; ++bb) {
-                const int b = b0 + bb;
-                if (n >= s_we[b]) continue;
-                double2 acc = c_zero();
-#pragma unroll
-                for (int j0 = 0; j0 < KPER; j0 += 16) {
-                    // at most 16 row values in flight (chi = 128: 32 would add 128 VGPRs to the slice's 128)
-#pragma unroll
-                    for (int jj = j0; jj < j0 + 16 && jj < KPER; ++jj)
-                        c_fma(acc, smem[L::PRO + b * CHI + kq * KPER + jj], sreg[jj]);
-                    if (KPER > 16) asm volatile("" ::: "memory");
-                }
-                smem[L::REDO + bb * NT + tid] = acc;
-            }
-            __syncthreads();
-            if (b0 == 0 && n >= 1) flush(n);
-            for (int e = tid; e < nb * CHI; e += NT) {
-                const int bb = e / CHI, d = e - bb * CHI, b = b0 + bb;
-                if (n >= s_we[b]) continue;
-                double2 y = smem[L::REDO + bb * NT + d];
-#pragma unroll
-                for (int k2 = 1; k2 < KG; ++k2) y = c_add(y, smem[L::REDO + bb * NT + k2 * CHI + d]);
-                ms_st_sc1(Xg + ((size_t)b * 2 + (n & 1)) * E + (size_t)g * CHI + d, y);
-            }
-            if (b0 + L::TBC < TB) __syncthreads();  // REDO reused by the next pass
-        }
-        // ---- arrive (every storing wave drained, then one lane)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) __hip_atomic_store((mu32*)(ct + g), (unsigned)n + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // ---- operands of step m = n + 1: F rows, output rows, closure column, then the slice row
-        const int m = n + 1;
+    // every entry is written (out-of-range ones to a dummy slot): a load consumed on some paths only stays pending in
+    // the waitcnt pass across the loop, and a later wait for it would hold the gather's loads (vmcnt is in order)
+    auto stage_ops = [&]() {
 #pragma unroll
         for (int i = 0; i < L::FPT; ++i) {
             const int e = tid + NT * i;
-            if (e < TB * N2) {
-                const int b = e / N2, be = e - b * N2;
-                if (m < s_we[b]) {
-                    const int sy = s_sy[b];
-                    const double2* __restrict__ Fr =
-                        s_evs[b] == m ? q.Fev + (size_t)s_evi[b] * m2 : fw_F(p, sy, fw_win(p, sy), m, m2);
-                    fpre[i] = ms_gld(Fr + (size_t)g * N2 + be);
-                }
-            }
+            const int r = e / (TB * N2), be = e % (TB * N2);
+            smem[e < R * TB * N2 ? L::FRO + r * TBM * N2 + be : L::DUMMY] = fpre[i];
         }
-        const int wrow = n_out * N2;
 #pragma unroll
         for (int i = 0; i < L::WPT; ++i) {
             const int e = tid + NT * i;
-            const int mb = e / wrow, r = e - mb * wrow, b = g + N2 * mb;
-            if (mb < tmine && m >= s_wb[b] && m <= s_we[b]) {
-                const int sy = s_sy[b];
-                const double2* __restrict__ Wr =
-                    s_evs[b] == m ? q.Wev + (size_t)s_evi[b] * wrow : fw_W(p, sy, fw_win(p, sy), m, N2);
-                wpre[i] = ms_gld(Wr + r);
-            }
+            const int mb = e / wrow, rr = e - mb * wrow;
+            smem[mb < tmine ? L::WLO + (mb * L::OMAX) * N2 + rr : L::DUMMY] = wpre[i];
         }
-        const double2 cvr = ms_gld(p.closure + (size_t)cur_slice * CHI + kcol);  // sched[n]: the slice PT(n) used
-        if (m < n_end) {
-            if ((m & 63) == 0) { sch_cur = sch_nxt; sch_nxt = sched_chunk((m >> 6) + 1); }
-            const int ns = __builtin_amdgcn_readlane(sch_cur, m & 63);
+        smem[tid < CHI ? L::CLO + tid : L::DUMMY] = clv;
+    };
+    // outputs at step n: the CHI output columns the gather of step n - 1 left per (trajectory, output), summed by one
+    // wave each and stored. Run by waves 1.. while wave 0 polls (first = 1), or by every wave after the last step
+    auto flush = [&](int n, int first) {
+        const int nw = NW - first, w = (tid >> 6) - first;
+        for (int e = w; e < tmine * n_out; e += nw) {
+            const int mb = e / n_out, k = e - mb * n_out, b = g + G * mb;
+            if (n < s_wb[b] || n > s_we[b]) continue;
+            double2 o = lane < CHI ? smem[L::OPO + (mb * L::OMAX + k) * CHI + lane] : c_zero();
+            o = ms_wave_sum(o);
+            if (lane == 0) p.out[s_wo[b] + (long long)(n - s_wb[b]) * n_out + k] = o;
+        }
+    };
+    load_ops(1);
+    clv = ms_gld(p.closure + (size_t)(n_end > 0 ? cur_slice : 0) * CHI + (tid & (CHI - 1)));
+    __syncthreads();
+
+    for (int n = 0;; ++n) {
+        stamp(n, 0);
+        if (n >= n_end) {
+            __syncthreads();
+            if (n >= 1) flush(n, 0);
+            break;
+        }
+        const int m = n + 1;
+        const unsigned long long act = mask(n < my_we);                      // PT(n), published, gathered
+        const unsigned long long nxt = mask(m < my_we);                      // r_b for PT(m)
+        const unsigned long long own = mask(lane < TB && lane % G == g && m >= my_wb && m <= my_we);  // outputs at m
+        // ---- PT(n), half h: row alpha_h of every trajectory that continues past n, TBC at a time (LDS partials)
+        for (int b0 = 0; b0 < TB; b0 += L::TBC) {
+            const int nb = TB - b0 < L::TBC ? TB - b0 : L::TBC;
+            if (live) {
+                for (int bb = 0; bb < nb; ++bb) {
+                    const int b = b0 + bb;
+                    if (!((act >> b) & 1)) continue;
+                    // every row value in flight before the first product (one at a time, the broadcast LDS reads
+                    // were a chain of round trips: ≈1,600 cycles for 16 complex MACs, scripts/msplit_stamps.py)
+                    double2 acc = c_zero();
+#pragma unroll
+                    for (int j0 = 0; j0 < KPER; j0 += L::PRB) {
+                        double2 prv[L::PRB];
+#pragma unroll
+                        for (int jj = 0; jj < L::PRB; ++jj)
+                            prv[jj] = smem[L::PRO + (h * TBM + b) * CHI + kq * KPER + j0 + jj];
+#pragma unroll
+                        for (int jj = 0; jj < L::PRB; ++jj) c_fma(acc, prv[jj], sreg[j0 + jj]);
+                    }
+                    smem[L::REDO + (h * L::TBC + bb) * HT + ht] = acc;
+                }
+            }
+            __syncthreads();
+            if (b0 == 0) stamp(n, 1);
+            if (live) {
+                for (int e = ht; e < nb * CHI; e += HT) {
+                    const int bb = e / CHI, d = e - bb * CHI, b = b0 + bb;
+                    if (!((act >> b) & 1)) continue;
+                    double2 y = smem[L::REDO + (h * L::TBC + bb) * HT + d];
+#pragma unroll
+                    for (int k2 = 1; k2 < KG; ++k2) y = c_add(y, smem[L::REDO + (h * L::TBC + bb) * HT + k2 * CHI + d]);
+                    ms_st_sc1(Xg + ((size_t)b * 2 + (n & 1)) * E + (size_t)alpha * CHI + d, y);
+                }
+            }
+            if (b0 + L::TBC < TB) __syncthreads();  // REDO reused by the next pass
+        }
+        // ---- arrive (every storing wave drained, then one lane). The builtin tells the waitcnt pass that nothing is
+        // pending past this point (the operand loads of the last gather included); the asm keeps the wait where it is
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store((mu32*)(ct + g), (unsigned)n + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        stamp(n, 2);
+        // ---- operands of step n + 1 (loaded during step n - 1's gather) to LDS
+        stage_ops();
+        stamp(n, 3);
+        // step n + 2's operand loads, the closure column of the outputs at step n + 2 (the slice PT(n + 1) uses) and the
+        // slice rows of step n + 1 are issued in the gather, behind its first loads (the vmcnt waits are in order: issued
+        // here they would sit in front of the gather's)
+        // (all of them unconditional but the slice rows: a path with fewer loads after the gather's would make the
+        // waitcnt pass wait for the gather with a smaller count on every path)
+        auto issue_ops = [&]() {
+            if constexpr (STAMP) {  // timing-only ablations (results not used): 128 no operand loads, 256 no closure
+                if (!(p.ablate & 128)) load_ops(m + 1);
+            } else {
+                load_ops(m + 1);  // entries past their window read rho0[0]
+            }
+            const int ns = m < n_end ? __builtin_amdgcn_readlane(sch_reg, m & 63) : cur_slice;
+            sch_reg = sched_chunk((m + 1) >> 6);
+            clv = ms_gld(p.closure + (size_t)ns * CHI + (tid & (CHI - 1)));
             if (ns != cur_slice) {
                 fetch_slice(ns);
                 cur_slice = ns;
             }
-        }
-#pragma unroll
-        for (int i = 0; i < L::FPT; ++i) {
-            const int e = tid + NT * i;
-            if (e < TB * N2) smem[L::FRO + e] = fpre[i];
-        }
-#pragma unroll
-        for (int i = 0; i < L::WPT; ++i) {
-            const int e = tid + NT * i;
-            const int mb = e / wrow, r = e - mb * wrow;
-            if (mb < tmine) smem[L::WLO + (mb * L::OMAX) * N2 + r] = wpre[i];
-        }
-        // ---- wait for the group
+        };
+        // ---- wait for the group (wave 0); the other waves store the outputs of step n meanwhile
+        if (tid >= 64 && n >= 1) flush(n, 1);
         if (tid < 64) {
             const unsigned want = (unsigned)n + 1u;
             unsigned spins = 0;
             bool ok = true;
             for (;;) {
                 const unsigned v =
-                    lane < N2 ? __hip_atomic_load((mu32*)(ct + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : want;
+                    lane < G ? __hip_atomic_load((mu32*)(ct + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : want;
                 if (__all(v >= want)) break;
                 __builtin_amdgcn_s_sleep(1);
                 if (++spins > p.spin_limit) { ok = false; break; }
@@ -307,60 +432,91 @@ __global__ __launch_bounds__(4 * CHI) void pt_msplit_kernel(SweepParams p, Mspli
         }
         __syncthreads();
         if (s_abort) return;
+        stamp(n, 4);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: payload loads are sc1
-        // composites of step m consumed (every reader of s_evs for m ran before the barrier above)
-        if (tid < TB && s_evs[tid] == m) {
-            const int i = ++s_evi[tid];
-            s_evs[tid] = i < s_eve[tid] ? q.cev[i].x : INT_MAX;
-        }
-        // ---- gather slot n & 1: r_b(m) into PRO, output partials of this workgroup's trajectories
-        for (int b0 = 0; b0 < TB; b0 += L::GCH) {
-            v4u32m xr[L::GCH][EPT];
+        // ---- gather slot n & 1, half h: trajectories b = h + R i; r_b^{r}(m) for the R rows into PRO, output partials
+        // of this workgroup's trajectories
+        // the first chunk is peeled (first = true: the operand loads are issued behind its gather loads); a loop body
+        // shared by chunks with and without those loads would wait for the gather with the smaller count
+        const double2 cv = smem[L::CLO + kcol];
+        auto chunk = [&](auto gct, auto firstt, int b0) {
+            constexpr int GC = decltype(gct)::value;
+            constexpr bool FIRST = decltype(firstt)::value != 0;
+            // every slot's loads are issued and waited for on every path (an idle slot reads element 0, one line for the
+            // whole wave): loads that are consumed on some paths only stay pending in the waitcnt pass across the loops,
+            // and the waits it then puts in front of the next chunk's loads serialised the chunk's round trips
+            v4u32m xr[GC][EPT];
 #pragma unroll
-            for (int bb = 0; bb < L::GCH; ++bb) {
-                const int b = b0 + bb;
-                if (b < TB && n < s_we[b]) {
+            for (int bb = 0; bb < GC; ++bb) {
+                const int b = b0 + R * bb;
+                const bool on = b < TB && ((act >> b) & 1);
 #pragma unroll
-                    for (int i = 0; i < EPT; ++i) {
-                        const int be = rg + RG * i;
-                        const int off = (int)((((size_t)b * 2 + (n & 1)) * E + (size_t)(be < N2 ? be : 0) * CHI + kcol) * 16);
-                        xr[bb][i] = __builtin_amdgcn_raw_buffer_load_b128(rX, off, 0, 16);
-                    }
+                for (int i = 0; i < EPT; ++i) {
+                    const int be = rg + RG * i;
+                    const int off = on ? (int)((((size_t)b * 2 + (n & 1)) * E + (size_t)(be < N2 ? be : 0) * CHI + kcol) * 16)
+                                       : 0;
+                    xr[bb][i] = __builtin_amdgcn_raw_buffer_load_b128(rX, off, 0, 16);
                 }
             }
+            if constexpr (FIRST) {
+                __builtin_amdgcn_sched_barrier(0);
+                issue_ops();
+                __builtin_amdgcn_sched_barrier(0);
+                stamp(n, 5);
+            }
 #pragma unroll
-            for (int bb = 0; bb < L::GCH; ++bb) {
-                const int b = b0 + bb;
-                if (b >= TB || n >= s_we[b]) continue;
+            for (int bb = 0; bb < GC; ++bb)
+#pragma unroll
+                for (int i = 0; i < EPT; ++i) asm volatile("" ::"v"(xr[bb][i]));
+#pragma unroll
+            for (int bb = 0; bb < GC; ++bb) {
+                const int b = b0 + R * bb;
+                if (b >= TB || !((act >> b) & 1)) continue;
                 double2 xv[EPT];
 #pragma unroll
                 for (int i = 0; i < EPT; ++i)
                     xv[i] = make_double2(__hiloint2double((int)xr[bb][i].y, (int)xr[bb][i].x),
                                          __hiloint2double((int)xr[bb][i].w, (int)xr[bb][i].z));
-                if (m < s_we[b]) {
-                    double2 part = c_zero();
+                if ((nxt >> b) & 1) {
 #pragma unroll
-                    for (int i = 0; i < EPT; ++i)
-                        if (rg + RG * i < N2) c_fma(part, smem[L::FRO + b * N2 + rg + RG * i], xv[i]);
-                    part = c_group_sum<4>(part);
-                    if (rg == 0) smem[L::PRO + b * CHI + kcol] = part;
+                    for (int r = 0; r < R; ++r) {
+                        if (R * g + r >= N2) continue;
+                        double2 part = c_zero();
+#pragma unroll
+                        for (int i = 0; i < EPT; ++i)
+                            if (rg + RG * i < N2) c_fma(part, smem[L::FRO + (r * TBM + b) * N2 + rg + RG * i], xv[i]);
+                        part = c_group_sum<4>(part);
+                        if (rg == 0) smem[L::PRO + (r * TBM + b) * CHI + kcol] = part;
+                    }
                 }
-                if (b % N2 == g && m >= s_wb[b]) {
-                    const int mb = b / N2;
-#pragma unroll
-                    for (int i = 0; i < EPT; ++i) xv[i] = c_mul(xv[i], cvr);
+                if ((own >> b) & 1) {
+                    // output column kcol of W(m)[k] . Q times the closure: like a row of r_b, the sum over columns
+                    // is left to flush (next step, while wave 0 polls)
+                    const int mb = b / G;
                     for (int k = 0; k < n_out; ++k) {
                         double2 o = c_zero();
 #pragma unroll
                         for (int i = 0; i < EPT; ++i)
                             if (rg + RG * i < N2) c_fma(o, smem[L::WLO + (mb * L::OMAX + k) * N2 + rg + RG * i], xv[i]);
-                        o = ms_wave_sum(o);
-                        if (lane == 0) smem[L::OPO + (mb * L::OMAX + k) * NW + wv] = o;
+                        o = c_group_sum<4>(o);
+                        if (rg == 0) smem[L::OPO + (mb * L::OMAX + k) * CHI + kcol] = c_mul(o, cv);
                     }
                 }
             }
+                };
+        // the first chunk is peeled and sized to the half's trajectories (idle slots still cost their loads' issue)
+        const int nh = h < TB ? (TB - h + R - 1) / R : 0;  // trajectories of this half
+        int fc = 0;
+        if constexpr (L::GCH >= 4) {
+            if (nh >= 4) { chunk(MsIC<4>{}, MsIC<1>{}, h); fc = 4; }
         }
-        if constexpr (CHI > 64) __syncthreads();  // a k-group spans two waves: r_b from both before PT(m)
+        if (fc == 0 && nh >= 2 && L::GCH >= 2) { chunk(MsIC<(L::GCH >= 2 ? 2 : 1)>{}, MsIC<1>{}, h); fc = L::GCH >= 2 ? 2 : 1; }
+        if (fc == 0 && nh >= 1) { chunk(MsIC<1>{}, MsIC<1>{}, h); fc = 1; }
+        if (fc == 0) issue_ops();
+        for (int b0 = h + R * fc; b0 < TB; b0 += R * L::GCH) chunk(MsIC<L::GCH>{}, MsIC<0>{}, b0);
+        stamp(n, 6);
+        __syncthreads();  // r_b from every half before PT(m)
+        stamp(n, 7);
     }
 }
 
@@ -401,57 +557,68 @@ __global__ __launch_bounds__(256) void evcomp_kernel(SweepParams p, MsplitParams
             for (int b = 0; b < N2; ++b) c_fma(acc, ms_gld(p.ovec + (size_t)k * N2 + b), P[b * N2 + c]);
             q.Wev[(size_t)e * p.n_out * N2 + i] = acc;
         }
-        double2* R = P == A ? Cm : A;  // the free buffer
+        double2* Rb = P == A ? Cm : A;  // the free buffer
         if (ce.z >= 0) {
             __syncthreads();
             for (int i = tid; i < m2; i += 256) B[i] = ms_gld(p.sop + (size_t)ce.z * m2 + i);
             __syncthreads();
-            mul(B, P, R);
-            double2* t = P; P = R; R = t;
+            mul(B, P, Rb);
+            double2* t = P; P = Rb; Rb = t;
         }
         __syncthreads();
         for (int i = tid; i < m2; i += 256) B[i] = s < n_steps ? ms_gld(fw_M(p, sy, wn, 2 * s, m2) + i) : c_zero();
         __syncthreads();
-        mul(B, P, R);
-        for (int i = tid; i < m2; i += 256) q.Fev[(size_t)e * m2 + i] = R[i];
+        mul(B, P, Rb);
+        for (int i = tid; i < m2; i += 256) q.Fev[(size_t)e * m2 + i] = Rb[i];
     }
 }
 
-template <int N2, int CHI>
+template <int N2, int CHI, int R, bool STAMP = false>
 hipError_t launch_ms_t(const SweepParams& p, const MsplitParams& q, double2* X, unsigned* cnt, unsigned* err,
-                       int n_blocks, hipStream_t s) {
-    using L = MsLayout<N2, CHI>;
+                       hipStream_t s) {
+    using L = MsLayout<N2, CHI, R>;
+    if constexpr (!STAMP && N2 == 16 && CHI == 64) {
+        if (p.ablate & 64) return launch_ms_t<N2, CHI, R, true>(p, q, X, cnt, err, s);
+    }
     static unsigned attr = 0;  // per-device bitmask
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
-    if (dev < 32 && !(attr & (1u << dev))) {
-        hipError_t e = hipFuncSetAttribute((const void*)pt_msplit_kernel<N2, CHI>,
+    if (dev >= 32 || !(attr & (1u << dev))) {
+        hipError_t e = hipFuncSetAttribute((const void*)pt_msplit_kernel<N2, CHI, R, STAMP>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::LDS);
         if (e != hipSuccess) return e;
-        attr |= 1u << dev;
+        if (dev < 32) attr |= 1u << dev;
     }
-    hipLaunchKernelGGL((pt_msplit_kernel<N2, CHI>), dim3(n_blocks), dim3(L::NT), L::LDS, s, p, q, X, cnt, err);
+    const int n_blocks = q.xcd > 0 ? 8 * q.xcd * L::G : q.n_groups * L::G;
+    hipLaunchKernelGGL((pt_msplit_kernel<N2, CHI, R, STAMP>), dim3(n_blocks), dim3(L::NT), L::LDS, s, p, q, X, cnt,
+                       err);
     return hipGetLastError();
 }
 
-template <int N2, int CHI>
+template <int N2, int CHI, int R>
 int ms_occ_t() {
-    using L = MsLayout<N2, CHI>;
-    if (hipFuncSetAttribute((const void*)pt_msplit_kernel<N2, CHI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    using L = MsLayout<N2, CHI, R>;
+    if (hipFuncSetAttribute((const void*)pt_msplit_kernel<N2, CHI, R>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)L::LDS) != hipSuccess)
         return 0;
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, pt_msplit_kernel<N2, CHI>, L::NT, L::LDS) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, pt_msplit_kernel<N2, CHI, R>, L::NT, L::LDS) != hipSuccess)
         return 0;
     return nb;
 }
 
+// rows per workgroup: 2 (each trajectory's state gathered by half as many workgroups, the slice rows 128 KiB per CU
+// at chi = 64 in the registers of 512 threads), 1 at N2 = 9 (G = 9 keeps three groups per XCD)
+constexpr int ms_rows(int N2) { return N2 == 9 ? 1 : 2; }
+
 template <int N2>
 hipError_t launch_ms_n(int CHI, const SweepParams& p, const MsplitParams& q, double2* X, unsigned* cnt,
-                       unsigned* err, int n_blocks, hipStream_t s) {
+                       unsigned* err, hipStream_t s) {
     switch (CHI) {
-        case 32: return launch_ms_t<N2, 32>(p, q, X, cnt, err, n_blocks, s);
-        case 64: return launch_ms_t<N2, 64>(p, q, X, cnt, err, n_blocks, s);
+        case 32: return launch_ms_t<N2, 32, ms_rows(N2)>(p, q, X, cnt, err, s);
+        case 64:
+            if constexpr (N2 != 25) return launch_ms_t<N2, 64, ms_rows(N2)>(p, q, X, cnt, err, s);
+            return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
     }
 }
@@ -459,19 +626,24 @@ hipError_t launch_ms_n(int CHI, const SweepParams& p, const MsplitParams& q, dou
 template <int N2>
 int ms_occ_n(int CHI) {
     switch (CHI) {
-        case 32: return ms_occ_t<N2, 32>();
-        case 64: return ms_occ_t<N2, 64>();
+        case 32: return ms_occ_t<N2, 32, ms_rows(N2)>();
+        case 64:
+            if constexpr (N2 != 25) return ms_occ_t<N2, 64, ms_rows(N2)>();
+            return 0;
         default: return 0;
     }
 }
 
 }  // namespace
 
-int msplit_tbmax(int CHI) { return CHI == 128 ? 16 : 32; }
+int msplit_tbmax(int N2, int CHI) { (void)CHI; return ms_rows(N2) == 1 ? 32 : 16; }
+int msplit_cev_max() { return MS_CEV_MAX; }
+int msplit_group_size(int N2) { return (N2 + ms_rows(N2) - 1) / ms_rows(N2); }
 
 bool msplit_supported(int N2, int CHI, int n_out) {
-    return (N2 == 9 || N2 == 16 || N2 == 25 || N2 == 36) && (CHI == 32 || CHI == 64) &&
-           n_out >= 1 && n_out <= 8;
+    // N2 = 25 at chi = 64 spills (7 gathered rows per thread for two PT rows): the single split or batched kernels
+    return (N2 == 9 || N2 == 16 || N2 == 25 || N2 == 36) && (CHI == 32 || (CHI == 64 && N2 != 25)) && n_out >= 1 &&
+           n_out <= 8;
 }
 
 int msplit_blocks_per_cu(int N2, int CHI) {
@@ -504,12 +676,16 @@ hipError_t launch_msplit(int N2, int CHI, const SweepParams& p, const MsplitPara
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(err, 0, 4 * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
-    const int n_blocks = q.xcd > 0 ? 8 * q.xcd * N2 : q.n_groups * N2;
     switch (N2) {
-        case 9: return launch_ms_n<9>(CHI, p, q, X, cnt, err, n_blocks, s);
-        case 16: return launch_ms_n<16>(CHI, p, q, X, cnt, err, n_blocks, s);
-        case 25: return launch_ms_n<25>(CHI, p, q, X, cnt, err, n_blocks, s);
-        case 36: return launch_ms_n<36>(CHI, p, q, X, cnt, err, n_blocks, s);
+        case 9: return launch_ms_n<9>(CHI, p, q, X, cnt, err, s);
+        case 16: return launch_ms_n<16>(CHI, p, q, X, cnt, err, s);
+        case 25: return launch_ms_n<25>(CHI, p, q, X, cnt, err, s);
+        case 36: return launch_ms_n<36>(CHI, p, q, X, cnt, err, s);
         default: return hipErrorInvalidValue;
     }
+}
+
+// diagnostics: the stamps of the last PQD_ABLATE=64 multi-trajectory split launch (2 workgroups x 16 steps x 8 phases)
+extern "C" int pqd_debug_msplit_stamps(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ms_stamps), sizeof(unsigned long long) * 256) == hipSuccess ? 0 : 4;
 }

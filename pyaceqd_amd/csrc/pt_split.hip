@@ -96,6 +96,9 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
     constexpr int OPO = 2 * E, RRO = OPO + N2 * N2, REDO = RRO + N2, CVO = REDO + SP_NT, WRO = CVO + CHI;
     constexpr int PRT = WRO + L::WST;  // counter form: KG partial sums of the next PT row (see the gather)
     constexpr int WST = L::WST, WPT = WST / SP_NT;
+    // chi = 64 fused gather: wave w writes PRT[16 w + lane] and only its own PT k-range (kq KPER ..) reads them, with no
+    // barrier between — that holds only while a wave's k-range is exactly those 16 columns
+    static_assert(CHI != 64 || (KG == 4 && KPER == 16 && SP_NT == 256), "PRT layout assumes one wave per k-group");
     __shared__ int s_abort;
     if (threadIdx.x == 0) s_abort = 0;
 
@@ -553,12 +556,14 @@ hipError_t launch_split_tg(int n_traj, const SweepParams& p, double2* X, unsigne
     if constexpr (!STAMP && !GRAN && N2 == 16 && CHI == 64) {
         if (p.ablate & 32) return launch_split_tg<N2, CHI, GRAN, OWG, true>(n_traj, p, X, cnt, err, s);
     }
-    static bool attr = false;
-    if (!attr) {
+    static unsigned attr = 0;  // per-device bitmask (a second device needs the attribute set too)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
+    if (dev >= 32 || !(attr & (1u << dev))) {
         hipError_t e = hipFuncSetAttribute((const void*)pt_split_kernel<N2, CHI, GRAN, OWG, STAMP>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::LDS);
         if (e != hipSuccess) return e;
-        attr = true;
+        if (dev < 32) attr |= 1u << dev;
     }
     // XCD-grouped grid when every XCD slot can hold its groups at one workgroup per CU (32 CUs per XCD on MI355X):
     // 8 slots x ceil(n_traj / 8) groups x G blocks, the blocks of missing groups return at once

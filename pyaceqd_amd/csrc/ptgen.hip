@@ -1596,18 +1596,41 @@ std::atomic<int> g_qr_fallbacks{0};   // persistent QRCP launches rerun one laun
 
 // scratch per (device, stream): a factorization's kernels stay queued after the call returns (pqd_ptg_qr without
 // pivoting does not synchronise), so a call on another stream or device must not reuse the same buffer.
-// Calls are serialised by g_mu; the buffer of a stream grows (after synchronising that stream) and is kept.
+// Calls are serialised by g_mu; the buffer of a stream grows (after synchronising that stream) and is kept. At most
+// SCR_KEEP buffers are kept: past that the least recently used one is freed after synchronising its device (its stream
+// handle may be gone by then), so a caller cycling through many streams does not accumulate buffers.
 std::mutex g_mu;
 struct Scratch {
     void* p = nullptr;
     size_t bytes = 0;
+    unsigned long long used = 0;
 };
 std::map<std::pair<int, hipStream_t>, Scratch> g_scr;
+unsigned long long g_scr_tick = 0;
+constexpr size_t SCR_KEEP = 8;
 hipError_t scratch(hipStream_t s, size_t bytes, void** out) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    Scratch& sc = g_scr[std::make_pair(dev, s)];
+    const auto key = std::make_pair(dev, s);
+    Scratch& sc = g_scr[key];
+    sc.used = ++g_scr_tick;
+    if (g_scr.size() > SCR_KEEP) {
+        auto lru = g_scr.end();
+        for (auto it = g_scr.begin(); it != g_scr.end(); ++it)
+            if (it->first != key && (lru == g_scr.end() || it->second.used < lru->second.used)) lru = it;
+        if (lru != g_scr.end()) {
+            if (lru->second.p) {
+                if ((e = hipSetDevice(lru->first.first)) != hipSuccess) return e;
+                e = hipDeviceSynchronize();
+                if (e == hipSuccess) e = hipFree(lru->second.p);
+                const hipError_t e2 = hipSetDevice(dev);
+                if (e != hipSuccess) return e;
+                if (e2 != hipSuccess) return e2;
+            }
+            g_scr.erase(lru);
+        }
+    }
     if (bytes > sc.bytes) {
         if (sc.p) {
             e = hipStreamSynchronize(s);

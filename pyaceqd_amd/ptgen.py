@@ -144,6 +144,48 @@ def _keep(S, threshold, max_k):
     return max(1, min(k, max_k) if max_k else k)
 
 
+class TruncationStats:
+    """What decided the boundary cuts of one generation: the caller's threshold keeps every
+    singular value above threshold x sigma_1 (ACE's `threshold`, general_system.py:159-190), the bond cap (the sweep
+    kernel's LDS bond, default_max_bond) may cut below that. Recorded per boundary SVD: how many cuts the cap made
+    (cap_bound), the largest rank the threshold asked for, and the largest discarded singular value relative to
+    sigma_1 (max_discarded_rel: at most the threshold where the threshold decided every cut)."""
+
+    def __init__(self, threshold, max_bond):
+        self.threshold, self.max_bond = float(threshold), max_bond
+        self.compressions = 0
+        self.cap_bound = 0
+        self.max_rank_wanted = 0
+        self.max_discarded_rel = 0.0
+
+    def record(self, S, k):
+        S = np.asarray(S)
+        if S.size == 0 or S[0] == 0:
+            return
+        self.compressions += 1
+        want = int(np.count_nonzero(S > self.threshold * S[0]))
+        self.max_rank_wanted = max(self.max_rank_wanted, want)
+        if self.max_bond and want > self.max_bond:
+            self.cap_bound += 1
+        if k < S.size:
+            self.max_discarded_rel = max(self.max_discarded_rel, float(S[k] / S[0]))
+
+    def as_meta(self):
+        return {"compressions": self.compressions, "cap_bound": self.cap_bound,
+                "max_rank_wanted": self.max_rank_wanted, "max_discarded_rel": self.max_discarded_rel,
+                "cap_decided": self.cap_bound > 0}
+
+    def warn(self, where):
+        """warnings.warn when the cap, not the threshold, set any cut"""
+        if self.cap_bound:
+            import warnings
+            warnings.warn(f"{where}: the bond cap {self.max_bond} (the sweep kernel's bond) cut {self.cap_bound} of "
+                          f"{self.compressions} boundary SVDs below the threshold {self.threshold:g}: the threshold "
+                          f"asked for bonds up to {self.max_rank_wanted}; largest discarded singular value "
+                          f"{self.max_discarded_rel:.2e} of sigma_1 (recorded in pt.meta['truncation'])",
+                          RuntimeWarning, stacklevel=3)
+
+
 def _fix_phase(U, Vh):
     """deterministic gauge: the largest-|.| entry of every left singular vector is real positive"""
     idx = np.argmax(np.abs(U), axis=0)
@@ -152,15 +194,18 @@ def _fix_phase(U, Vh):
     return U * ph.conj()[None, :], Vh * ph[:, None]
 
 
-def _compress(mps, threshold, max_bond, tail_threshold=None, tail_max_bond=None):
+def _compress(mps, threshold, max_bond, tail_threshold=None, tail_max_bond=None, stats=None):
     """mps[0] has the (stacked) left boundary as its left index. Returns (U, mps') with U the isometry of the
-    boundary SVD (left dim x new bond) and mps' the compressed tail whose left index is the new bond."""
+    boundary SVD (left dim x new bond) and mps' the compressed tail whose left index is the new bond. `stats`
+    (TruncationStats) records what decided the boundary cut."""
     tthr = threshold if tail_threshold is None else tail_threshold
     _rcanon(mps)
     T = mps[0]
     L, P, cr = T.shape
     U, S, Vh = np.linalg.svd(T.reshape(L, P * cr), full_matrices=False)
     k = _keep(S, threshold, max_bond)
+    if stats is not None:
+        stats.record(S, k)
     U, Vh = _fix_phase(U[:, :k], Vh[:k])
     cur = (S[:k, None] * Vh).reshape(k, P, cr)
     for j in range(len(mps) - 1):
@@ -255,6 +300,7 @@ class GaussianPTBuilder:
         self.newp = np.einsum("pq,aq->ap", Bm, dplus[:, -1, :]) if self.K else None              # (nl, P)
         self.tail = [self.one.reshape(1, P, 1).copy() for _ in range(self.K)]
         self.r = 1
+        self.trunc = TruncationStats(self.threshold, max_bond)
 
     def closure(self, tail=None):
         tail = self.tail if tail is None else tail
@@ -272,14 +318,14 @@ class GaussianPTBuilder:
         # s+ half: present site re-indexed by s-, futures k = 1..K-1 and the new site k = K times the s+ factor
         first = np.einsum("ims,bsc->ibmc", self.reindex, tail[0])              # (nl, r, nl, c1)
         st = _stack(first, tail[1:], self.Fp[:, : K - 1], self.newp)
-        Up, chain = _compress(st, self.threshold, self.max_bond, self.tail_threshold, self.tail_max_bond)
+        Up, chain = _compress(st, self.threshold, self.max_bond, self.tail_threshold, self.tail_max_bond, self.trunc)
         r1 = Up.shape[1]
         # s- half: project the present site onto s-, every future site (incl. the new one) times the s- factor
         pres = chain[0]                                                         # (r1, nl, c1)
         nxt = np.einsum("bpq,lqr->blpr", self.Fm[:, 0], chain[1])               # (nl, c1, P, c2)
         first = np.einsum("ibc,icpr->ibpr", pres.transpose(1, 0, 2), nxt)       # (nl, r1, P, c2)
         st = _stack(first, chain[2:], self.Fm[:, 1:K], None)
-        Um, tail2 = _compress(st, self.threshold, self.max_bond, self.tail_threshold, self.tail_max_bond)
+        Um, tail2 = _compress(st, self.threshold, self.max_bond, self.tail_threshold, self.tail_max_bond, self.trunc)
         return Up.reshape(nl, r, r1), Um.reshape(nl, r1, Um.shape[1]), tail2
 
     def _slice(self, Up, Um):
@@ -342,8 +388,9 @@ def build_gaussian_pt(boson_op, dt, eta, delta_pol=0.0, n_init=None, threshold=1
         Cp[s, : c.shape[0]] = c
     e0 = np.zeros(chi, dtype=np.complex128)
     e0[0] = 1.0
+    b.trunc.warn("ptgen")
     return ProcessTensor(Q=Qp, closure=Cp, closure0=e0, bond0=e0, gmap=b.gmap,
-                         n_init=n_init if repeat else S - 1, dt=dt)
+                         n_init=n_init if repeat else S - 1, dt=dt, meta={"truncation": b.trunc.as_meta()})
 
 
 def infinite_memory_steps(eta, boson_op, threshold):
@@ -385,6 +432,12 @@ def qd_phonon_eta(boson_op, dt, t_mem=20.48, ae=3.0, temperature=1.0, threshold=
         eta, _ = eta_coefficients(J, temperature, dt, k_cap, e_max=boson_e_max)
         n_mem, conv = infinite_memory_steps(eta, boson_op, threshold)
         info.update(k_cap=k_cap, converged=bool(conv))
+        if not conv:  # say it, not only in meta (a stand-in for ACE's use_Gaussian_infinite, parity unpinned)
+            import warnings
+            warnings.warn(f"use_infinite: the bath's eta_k tail stays above the threshold {threshold:g} up to the te "
+                          f"horizon, so the memory is truncated at K = {n_mem} steps (2 t_mem / dt); this is a "
+                          f"truncated-memory stand-in for ACE's use_Gaussian_infinite (parity unpinned)",
+                          RuntimeWarning, stacklevel=2)
     else:
         n_mem = max(1, int(round(t_mem / dt)))
     eta, delta = eta_coefficients(J, temperature, dt, n_mem, e_max=boson_e_max)
@@ -431,7 +484,8 @@ def qd_phonon_pt(boson_op, dt, t_mem=20.48, ae=3.0, temperature=1.0, threshold=1
     pt = build_gaussian_pt(boson_op, dt, eta, delta, n_init=n_init, threshold=threshold, max_bond=max_bond,
                            repeat=True, verbose=verbose)
     pt.meta = dict(generation_key(boson_op, dt, t_mem, ae, temperature, threshold, factor_ah, boson_e_max, J_file,
-                                  use_infinite, max_bond), generator="host", tail="svd", **info)
+                                  use_infinite, max_bond), generator="host", tail="svd", **info,
+                   truncation=(pt.meta or {}).get("truncation"))
     return pt
 
 

@@ -191,8 +191,9 @@ def _rcanon(mps):
         mps[j - 1] = torch.tensordot(mps[j - 1], Rc, dims=([2], [0]))
 
 
-def _compress(mps, threshold, max_bond, tail_threshold=None, tail_max_bond=None, tail="qrcp"):
-    """ptgen._compress on the device. Returns (U, mps') with U the phase-fixed isometry of the boundary SVD."""
+def _compress(mps, threshold, max_bond, tail_threshold=None, tail_max_bond=None, tail="qrcp", stats=None):
+    """ptgen._compress on the device. Returns (U, mps') with U the phase-fixed isometry of the boundary SVD; `stats`
+    (ptgen.TruncationStats) records what decided the boundary cut."""
     torch = _torch()
     tthr = threshold if tail_threshold is None else tail_threshold
     tm = _PHASES is not None
@@ -211,6 +212,8 @@ def _compress(mps, threshold, max_bond, tail_threshold=None, tail_max_bond=None,
         t2 = time.perf_counter()
     Sh = S.cpu().numpy()
     k = _keep(Sh, threshold, max_bond)
+    if stats is not None:
+        stats.record(Sh, k)
     U, Vh = _fix_phase(U[:, :k], Vh[:k])
     cur = (S[:k, None].to(Vh.dtype) * Vh).reshape(k, P, cr)
     for j in range(len(mps) - 1):
@@ -292,6 +295,7 @@ class GaussianPTBuilderGPU:
         self.newp = d(h.newp) if h.newp is not None else None
         self.tail = [d(t) for t in h.tail]
         self.r = 1
+        self.trunc = ptgen.TruncationStats(self.threshold, max_bond)
         self._ip = torch.as_tensor(self.pair_ip, device=self.dev)
         self._im = torch.as_tensor(self.pair_im, device=self.dev)
 
@@ -312,14 +316,14 @@ class GaussianPTBuilderGPU:
         first = torch.einsum("ims,bsc->ibmc", self.reindex, tail[0])
         st = _stack(first, tail[1:], self.Fp[:, : K - 1], self.newp)
         Up, chain = _compress(st, self.threshold, self.max_bond, self.tail_threshold, self.tail_max_bond,
-                              self.tail_mode)
+                              self.tail_mode, self.trunc)
         r1 = Up.shape[1]
         pres = chain[0]
         nxt = torch.einsum("bpq,lqr->blpr", self.Fm[:, 0], chain[1])
         first = torch.einsum("ibc,icpr->ibpr", pres.permute(1, 0, 2), nxt)
         st = _stack(first, chain[2:], self.Fm[:, 1:K], None)
         Um, tail2 = _compress(st, self.threshold, self.max_bond, self.tail_threshold, self.tail_max_bond,
-                              self.tail_mode)
+                              self.tail_mode, self.trunc)
         return Up.reshape(nl, r, r1), Um.reshape(nl, r1, Um.shape[1]), tail2
 
     def _slice(self, Up, Um):
@@ -385,8 +389,9 @@ def build_gaussian_pt_gpu(boson_op, dt, eta, delta_pol=0.0, n_init=None, thresho
         Cp[s, : c.shape[0]] = c
     e0 = np.zeros(chi, dtype=np.complex128)
     e0[0] = 1.0
+    b.trunc.warn("ptgen_gpu")
     return ProcessTensor(Q=Qp, closure=Cp, closure0=e0, bond0=e0, gmap=b.gmap,
-                         n_init=n_init if repeat else S - 1, dt=dt)
+                         n_init=n_init if repeat else S - 1, dt=dt, meta={"truncation": b.trunc.as_meta()})
 
 
 def qd_phonon_pt_gpu(boson_op, dt, t_mem=20.48, ae=3.0, temperature=1.0, threshold=1e-10, factor_ah=None,
@@ -404,5 +409,6 @@ def qd_phonon_pt_gpu(boson_op, dt, t_mem=20.48, ae=3.0, temperature=1.0, thresho
     pt = build_gaussian_pt_gpu(boson_op, dt, eta, delta, n_init=n_init, threshold=threshold, max_bond=max_bond,
                                repeat=True, verbose=verbose, tail=tail)
     pt.meta = dict(ptgen.generation_key(boson_op, dt, t_mem, ae, temperature, threshold, factor_ah, boson_e_max,
-                                        J_file, use_infinite, max_bond), generator="gpu", tail=tail, **info)
+                                        J_file, use_infinite, max_bond), generator="gpu", tail=tail, **info,
+                   truncation=(pt.meta or {}).get("truncation"))
     return pt

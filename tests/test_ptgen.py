@@ -94,6 +94,25 @@ def test_bond_cap_and_padding():
     assert pt.D == 4 and list(pt.gmap) == [0, 1, 2, 3]
 
 
+def test_truncation_record_says_when_the_cap_decided():
+    """every generated PT records what set its boundary cuts (pt.meta['truncation']): with a
+    cap below the threshold's rank the cap decided (warning raised, the largest discarded singular value far above
+    the threshold); without a cap the threshold decided every cut (largest discarded value <= threshold)"""
+    import warnings
+    eta, delta = ptgen.eta_coefficients(QDJ, 4.0, 0.1, 8)
+    with pytest.warns(RuntimeWarning, match="bond cap 16"):
+        capped = ptgen.build_gaussian_pt(np.diag([0.0, 1.0]), 0.1, eta, delta, threshold=1e-12, max_bond=16)
+    tc = capped.meta["truncation"]
+    assert tc["cap_decided"] and tc["cap_bound"] > 0 and tc["max_rank_wanted"] > 16
+    assert tc["max_discarded_rel"] > 1e-12
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", RuntimeWarning)
+        free = ptgen.build_gaussian_pt(np.diag([0.0, 1.0]), 0.1, eta, delta, threshold=1e-8, max_bond=0)
+    tf = free.meta["truncation"]
+    assert not tf["cap_decided"] and tf["cap_bound"] == 0 and tf["compressions"] == 2 * (2 * 8 + 1)
+    assert 0 < tf["max_discarded_rel"] <= 1e-8
+
+
 def test_driver_generates_and_caches_pt(tmp_path, monkeypatch):
     """system_ace_stream(phonons=True) without a PT file: generate from the ACE generate-file parameters, cache
     under the reference's name (+ .npz), reuse on the next call; J_to_file writes J(omega). (The driver generates on
