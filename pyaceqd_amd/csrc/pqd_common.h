@@ -295,7 +295,8 @@ bool sweep_supported(int N2, int CHI);
 // split groups carrying TB trajectories each (pt_msplit.hip)
 bool msplit_supported(int N2, int CHI, int n_out);
 int msplit_tbmax(int N2, int CHI);
-int msplit_group_size(int N2);  // workgroups per group (each owns up to R PT rows of every trajectory)
+int msplit_cev_max();  // composite MTO steps per group (held in LDS)
+int msplit_group_size(int N2, int CHI);  // workgroups per group (each owns up to R PT rows of every trajectory)
 int msplit_blocks_per_cu(int N2, int CHI);
 hipError_t launch_evcomp(int N2, const SweepParams& p, const MsplitParams& q, int n_cev, int n_steps, hipStream_t s);
 hipError_t launch_msplit(int N2, int CHI, const SweepParams& p, const MsplitParams& q, double2* X, unsigned* cnt,

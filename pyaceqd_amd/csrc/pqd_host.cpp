@@ -894,7 +894,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
         const int bpc = (pt && !P->split && mode != 0 && fuse_on && tr->n_traj >= 1 && msplit_supported(N2, P->CHI, n_out))
                             ? msplit_blocks_per_cu(N2, P->CHI) : 0;
         if (bpc >= 1) {
-            const int G = msplit_group_size(N2);
+            const int G = msplit_group_size(N2, P->CHI);
             const int resident = n_cu * bpc / G;          // groups the device holds at once
             const int gps = 32 / G;                        // groups per XCD slot (32 CUs per XCD on MI355X)
             const int max_groups = std::min(resident, gps >= 1 ? 8 * gps : resident);
@@ -905,15 +905,31 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
             // (DESIGN.md §4.10); the single-trajectory groups keep the batches they fit
             // and while shared trunks would save little: the batched sweep starts each slot at its branch step (a
             // G2_reuse grid saves about half of its steps there), a split group runs every trajectory from step 0
+            // (a system's trunk itself is propagated once: what sharing saves is the activations beyond its longest)
             int64_t shared = 0, total = 0;
+            std::vector<int> amax(n_sys, 0);
             for (int t = 0; t < tr->n_traj; ++t) {
-                shared += std::max(0, std::min(jv[t], tr->out_begin[t]));
+                const int a = std::max(0, std::min(jv[t], tr->out_begin[t]));
+                shared += a;
+                amax[tsys[t]] = std::max(amax[tsys[t]], a);
                 total += tr->out_end[t] + 1;
             }
+            for (int y = 0; y < n_sys; ++y) shared -= amax[y];
             // (measured, profiles/r06/: 32 trajectories TB = 1 33 ms vs 124 ms batched; 256 trajectories TB = 8 114 vs
             // 124 ms; past TB = 8 the per-step gather of TB states per workgroup is not measured to win)
             const bool want = mode == 2 || (TB <= 8 && 4 * shared <= total);
-            if (want && TB <= msplit_tbmax(N2, P->CHI) && n_groups <= resident) {
+            // a group's composite MTO steps are held in LDS (pt_msplit.hip s_cev): at most msplit_cev_max() per group
+            int max_cev = 0;
+            for (int k0 = 0; k0 < tr->n_traj; k0 += TB) {
+                int c = 0;
+                for (int k = k0; k < std::min(tr->n_traj, k0 + TB); ++k) {
+                    const int t = order[k];
+                    for (int i = ev_start[t]; i < ev_start[t + 1]; ++i)
+                        if (i == ev_start[t] || evs[i].x != evs[i - 1].x) ++c;
+                }
+                max_cev = std::max(max_cev, c);
+            }
+            if (want && TB <= msplit_tbmax(N2, P->CHI) && n_groups <= resident && max_cev <= msplit_cev_max()) {
                 P->msplit = true;
                 ms_TB = TB;
                 ms_groups = n_groups;

@@ -76,9 +76,9 @@ struct MsLayout {
     static constexpr int G = (N2 + R - 1) / R;      // workgroups per group
     static constexpr int RG = 4;                    // gather row groups: lanes 4 c + rg of a k-group
     static constexpr int EPT = (N2 + RG - 1) / RG;  // state rows per thread and trajectory in the gather
-    static constexpr int GCH = R >= 4 ? 2 : (EPT <= 4 ? 4 : 1);  // trajectories per half with gather loads in flight
-    static constexpr int PRB = R >= 4 ? 4 : KPER;  // row values in flight in the PT (R = 4: 128 registers per thread)
-    static constexpr int TBMAX = R == 1 ? 32 : (R == 2 ? 16 : 8);
+    static constexpr int GCH = CHI > 64 ? 1 : (R >= 4 ? 2 : (EPT <= 4 ? 4 : 1));  // trajectories per half with gather loads in flight
+    static constexpr int PRB = (R >= 4 || CHI > 64) ? 4 : KPER;  // row values in flight in the PT (R = 4: 128 registers per thread)
+    static constexpr int TBMAX = CHI > 64 ? 8 : (R == 1 ? 32 : (R == 2 ? 16 : 8));
     static constexpr int TBC = R >= 4 ? 4 : 8;      // trajectories per PT pass (LDS partials)
     static constexpr int OMAX = 8;                  // outputs per trajectory
     static constexpr int TMINE = (TBMAX + G - 1) / G;  // trajectories whose outputs one workgroup writes
@@ -213,8 +213,11 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
     if (tid == 0) {
         int o = 0;
         for (int b = 0; b < TB; ++b) { s_cvo[b] = o; o += s_eve[b] - s_evi[b]; }
+        s_abort = o > MS_CEV_MAX;  // the host never launches such a group (msplit_cev_max); refuse rather than overrun
+        if (s_abort) __hip_atomic_store((mu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
+    if (s_abort) return;
     for (int b = 0; b < TB; ++b)
         for (int i = tid; i < s_eve[b] - s_evi[b]; i += NT) s_cev[s_cvo[b] + i] = q.cev[s_evi[b] + i].x;
     __syncthreads();
@@ -327,7 +330,9 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
         for (int e = w; e < tmine * n_out; e += nw) {
             const int mb = e / n_out, k = e - mb * n_out, b = g + G * mb;
             if (n < s_wb[b] || n > s_we[b]) continue;
-            double2 o = lane < CHI ? smem[L::OPO + (mb * L::OMAX + k) * CHI + lane] : c_zero();
+            double2 o = c_zero();
+#pragma unroll
+            for (int c = lane; c < CHI; c += 64) o = c_add(o, smem[L::OPO + (mb * L::OMAX + k) * CHI + c]);
             o = ms_wave_sum(o);
             if (lane == 0) p.out[s_wo[b] + (long long)(n - s_wb[b]) * n_out + k] = o;
         }
@@ -619,6 +624,9 @@ hipError_t launch_ms_n(int CHI, const SweepParams& p, const MsplitParams& q, dou
         case 64:
             if constexpr (N2 != 25) return launch_ms_t<N2, 64, ms_rows(N2)>(p, q, X, cnt, err, s);
             return hipErrorInvalidValue;
+        case 128:
+            if constexpr (N2 <= 16) return launch_ms_t<N2, 128, 1>(p, q, X, cnt, err, s);
+            return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
     }
 }
@@ -630,20 +638,26 @@ int ms_occ_n(int CHI) {
         case 64:
             if constexpr (N2 != 25) return ms_occ_t<N2, 64, ms_rows(N2)>();
             return 0;
+        case 128:
+            if constexpr (N2 <= 16) return ms_occ_t<N2, 128, 1>();
+            return 0;
         default: return 0;
     }
 }
 
 }  // namespace
 
-int msplit_tbmax(int N2, int CHI) { (void)CHI; return ms_rows(N2) == 1 ? 32 : 16; }
+int msplit_rows(int N2, int CHI) { return CHI > 64 ? 1 : ms_rows(N2); }
+int msplit_tbmax(int N2, int CHI) { return CHI > 64 ? 8 : (ms_rows(N2) == 1 ? 32 : 16); }
 int msplit_cev_max() { return MS_CEV_MAX; }
-int msplit_group_size(int N2) { return (N2 + ms_rows(N2) - 1) / ms_rows(N2); }
+int msplit_group_size(int N2, int CHI) { return (N2 + msplit_rows(N2, CHI) - 1) / msplit_rows(N2, CHI); }
 
 bool msplit_supported(int N2, int CHI, int n_out) {
     // N2 = 25 at chi = 64 spills (7 gathered rows per thread for two PT rows): the single split or batched kernels
-    return (N2 == 9 || N2 == 16 || N2 == 25 || N2 == 36) && (CHI == 32 || (CHI == 64 && N2 != 25)) && n_out >= 1 &&
-           n_out <= 8;
+    // chi = 128 (the bond cap of generated N <= 4 PTs, which the single-trajectory split kernel does not take): one PT
+    // row per workgroup of 512 threads, the 256 KiB slice row in their registers
+    return (N2 == 9 || N2 == 16 || N2 == 25 || N2 == 36) &&
+           (CHI == 32 || (CHI == 64 && N2 != 25) || (CHI == 128 && N2 <= 16)) && n_out >= 1 && n_out <= 8;
 }
 
 int msplit_blocks_per_cu(int N2, int CHI) {

@@ -13,6 +13,8 @@ algorithmic flops (fused half steps: F = 8 (D chi^2 + chi N^4 + n_out N^2), D = 
   c4reuse G2_reuse-shaped biexciton sweep (reference pol_entanglement/G2.py:486-497): 8 scan points x 1024 t1 points
           spread over [0, tend), every trajectory from step 0 to tend = 4,096 steps with its MTOs at t1, chi = 64;
           run without (PQD_BRANCH=0) and with shared trunks: executed vs useful traj-steps and wall per launch
+  c3one128 the single biexciton run on a chi = 128 dictionary PT (a generated PT's bond cap): split groups of one
+          PT row per workgroup (pt_msplit.hip) where the single-trajectory split kernel stops at chi = 64
   c4d128  the bench workload (8 scan points x 256 t1 x 10,000 tau, biexciton) on a synthetic chi = 128 dictionary PT
           (9 slices for the 16 rows: the shape of a generated biexciton PT at the reference parameters)
   c4g     the same workload on a GPU-generated biexciton PT at dt = 0.1 and the reference's biexciton parameters
@@ -141,6 +143,7 @@ CONFIGS = {
     "c5d": dict(model="sixls", n_scan=32, n_t1=64, n_tau=2000, chi=64, dictionary=True),
     "c3d": dict(model="biexciton", n_scan=8, n_t1=256, n_tau=2000, chi=64, dictionary=True),
     "c4d128": dict(model="biexciton", n_scan=8, n_t1=256, n_tau=10000, chi=128, dictionary=True),
+    "c3one128": dict(model="biexciton", n_scan=1, n_t1=1, n_tau=10000, chi=128, dictionary=True),
     "c4d128s": dict(model="biexciton", n_scan=8, n_t1=256, n_tau=2000, chi=128, dictionary=True),
     "c4g": dict(model="biexciton", n_scan=8, n_t1=256, n_tau=10000, chi=128, generated=True),
     "c4g2k": dict(model="biexciton", n_scan=8, n_t1=256, n_tau=2000, chi=128, generated=True),
@@ -173,6 +176,7 @@ def run(name, steps):
     F = 8 * (N * N * chi * chi + chi * N ** 4 + len(ops) * N * N) if chi > 1 else 8 * (N ** 4 + len(ops) * N * N)
     tf = executed * F / (ms_sweep * 1e-3) / 1e12
     return {"config": name, **cfg, "N": N, "n_traj": tr.n_traj, "executed_traj_steps": executed,
+            "path": plan.info()[0], "traj_per_group_or_block": plan.info()[1],
             "wall_ms_per_launch": el * 1e3, "pt_sweep_ms": ms_sweep, "free_prop_ms": ms_free,
             "traj_steps_per_s": executed / el, "flop_per_traj_step": F, "sweep_TFLOPs": tf, "frac_fp64": tf / PEAK,
             **extra}

@@ -117,6 +117,25 @@ def test_msplit_matches_batched_at_c4_shard_length(monkeypatch):
     cmp_lists(got, ref.download(), 1e-10)
 
 
+@pytest.mark.parametrize("N,n_traj", [(3, 1), (4, 1), (4, 7)])
+def test_msplit_chi128_vs_oracle(N, n_traj):
+    """chi = 128 (a generated PT's bond cap at N <= 4, which the single-trajectory split kernel does not take): auto
+    mode runs it on multi-trajectory split groups of one PT row per workgroup (a chi = 128 single
+    run on the split path), vs the oracle"""
+    systems = [H.random_system(N, n_steps=30, seed=80 + k)[0] for k in range(2)]
+    grid = Grid(0.0, 0.1, 30)
+    tr = mixed_trajectories(grid.n_steps, N, n_traj, seed=N + 128)
+    tr.system = np.array([k % 2 for k in range(n_traj)])
+    pt = ptmod.random_pt(N, 100, D=min(N * N, 9), n_slices=7, seed=N, eps=0.15)
+    ops = [H.ketbra(N, 0, 0), H.ketbra(N, 1, 0), np.eye(N)]
+    rho0 = H.random_rho(N)
+    plan = engine.Plan(systems, grid, rho0, ops, tr, pt=pt)
+    plan.execute()
+    got = plan.download()
+    assert plan.info()[0] == MSPLIT and plan.info()[2] == 0
+    cmp_lists(got, oracle.propagate(systems, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
+
+
 def test_msplit_timeout_falls_back_to_batched(monkeypatch):
     """PQD_SPLIT_SPIN=0: every wait for a peer times out; the plan re-runs the sweep on the batched kernel"""
     N, chi = 4, 64
