@@ -281,6 +281,38 @@ def run_c4_literal(steps, n_t1=256, t1_offset=0, name="c4full", cpu=True):
     return row
 
 
+def run_c4_ntraj(steps, n_tau=2000, sizes=(16, 24, 32, 48, 64, 96, 128, 192, 256, 384, 512)):
+    """where the multi-trajectory split groups stop paying: the C4 sweep shape (bench.build_workload, one scan point,
+    chi = 64, n_tau = 2,000) at growing t1 counts, on split groups forced (PQD_MSPLIT=2, past the auto cutoff) and on
+    the batched kernel (PQD_MSPLIT=0); sweep ms per launch and the path each took"""
+    import bench
+    from pyaceqd_amd import engine
+    rows = []
+    for n in sizes:
+        sysd, grid, pt, rho0, ops, tr = bench.build_workload(n, n_tau, 64)
+        row = {"n_traj": n, "grid_steps": grid.n_steps}
+        for label, env in (("msplit", {"PQD_MSPLIT": "2"}), ("auto", {}), ("batched", {"PQD_MSPLIT": "0"})):
+            for k, v in env.items():
+                os.environ[k] = v
+            try:
+                plan = engine.Plan(sysd, grid, rho0, ops, tr, pt=pt)
+            finally:
+                for k in env:
+                    os.environ.pop(k)
+            plan.execute()
+            plan.synchronize()
+            plan.timing(reset=True)
+            for _ in range(steps):
+                plan.execute()
+            plan.synchronize()
+            _, ms, _ = plan.timing(reset=True)
+            path, bt, _ = plan.info()
+            row[label] = {"path": path, "bt": bt, "sweep_ms": ms, "us_per_step": ms * 1e3 / (grid.n_steps + 1)}
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+    return {"config": "c4ntraj", "n_tau": n_tau, "rows": len(rows)}
+
+
 def run_c5dm(steps, n_e0=2, bxs=(0.0, 1.0, 2.0, 4.0), tend=400.0):
     import tempfile
     from pyaceqd_amd import opgrammar, pt as ptmod
@@ -324,7 +356,7 @@ def main():
     for name in args.configs.split(","):
         # c5dm32: one rank's share of SURVEY §8d C5 (256 points = 64 e0 x 4 bx over 8 GPUs): 8 e0 x 4 bx
         special = {"c5dm": run_c5dm, "c4reuse": run_c4reuse, "c5dm32": lambda st: run_c5dm(st, n_e0=8),
-                   "c4full": run_c4_literal,
+                   "c4full": run_c4_literal, "c4ntraj": run_c4_ntraj,
                    "c4shard": lambda st: run_c4_literal(st, n_t1=32, t1_offset=96, name="c4shard")}
         print(json.dumps(special[name](args.steps) if name in special else run(name, args.steps)), flush=True)
 
