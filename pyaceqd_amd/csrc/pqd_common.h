@@ -170,6 +170,7 @@ struct MsplitParams {
     double2* Wev;            // [n_cev][n_out][N2]: ovec S_before M_b(s - 1)
     int TB, n_groups;        // trajectories per group, groups
     int xcd;                 // > 0: XCD-grouped grid with this many groups per XCD slot; 0: plain grid
+    int l2keep;              // 1: payload stores keep their L2 lines (XCD-grouped grid only; placement checked in-kernel)
 };
 
 // ---- free propagators through the pulse windows: M(h), F(n) = M(2n) M(2n-1) and W(n) = ovec . M(2n-1) of system sys

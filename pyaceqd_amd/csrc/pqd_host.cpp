@@ -1196,8 +1196,10 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
         HIPCHK(P->msX.alloc((size_t)ms_groups * ms_TB * 2 * N2 * P->CHI));
         HIPCHK(P->ms_cnt.alloc((size_t)ms_groups * 64));
         HIPCHK(P->err.alloc(4));
+        // L2-kept exchange lines on the XCD-grouped grid (PQD_MS_L2=0: sc1 stores, as on the plain grid)
+        const int l2keep = ms_xcd > 0 && [] { const char* f = getenv("PQD_MS_L2"); return f ? atoi(f) != 0 : true; }();
         P->mq = MsplitParams{P->ms_gtraj.p, P->ms_gend.p, P->cev_start.p, P->cev.p, P->Fev.p, P->Wev.p,
-                             ms_TB, ms_groups, ms_xcd};
+                             ms_TB, ms_groups, ms_xcd, l2keep};
     }
     HIPCHK(hipStreamSynchronize(s));
     *out = guard.release();
@@ -1266,10 +1268,19 @@ int pqd_plan_synchronize(pqd_plan* P) {
         }
     }
     if (P->split || P->msplit) {
-        unsigned err = 0;
-        HIPCHK(hipMemcpyAsync(&err, P->err.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+        unsigned err[2] = {0, 0};
+        HIPCHK(hipMemcpyAsync(err, P->err.p, 2 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        if (err) {
+        if (err[0] && err[1] && P->msplit && P->mq.l2keep) {
+            // a group's workgroups were not all on one XCD (pt_msplit.hip l2keep): again with sc1 exchange stores,
+            // which need no placement, and stay there
+            P->mq.l2keep = 0;
+            P->split_fallbacks++;
+            HIPCHK(launch_msplit(P->N2, P->CHI, P->sp, P->mq, P->msX.p, P->ms_cnt.p, P->err.p, s));
+            HIPCHK(hipMemcpyAsync(err, P->err.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+        }
+        if (err[0]) {
             P->split = false;
             P->msplit = false;
             P->split_fallbacks++;

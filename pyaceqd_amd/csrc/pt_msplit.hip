@@ -42,6 +42,9 @@ typedef unsigned int v4u32m __attribute__((ext_vector_type(4)));
 
 constexpr int MS_LDS_FORCE = 96 * 1024;  // dynamic LDS request: one workgroup per CU
 constexpr int MS_CEV_MAX = 512;          // composite events per group held in LDS (msplit_cev_max)
+constexpr unsigned MS_STEP_MASK = 0x0FFFFFFFu;  // arrival word: step n + 1 in bits 0..27, the writer's XCD id above
+// s_getreg_b32 hwreg(HW_REG_XCC_ID, 0, 4): register id 20, offset 0, size 4 (simm16 = (size - 1) << 11 | offset << 6 | id)
+constexpr int MS_HWREG_XCC_ID = (3 << 11) | (0 << 6) | 20;
 template <int V>
 struct MsIC {  // compile-time int tag (the gather's chunk variants)
     static constexpr int value = V;
@@ -52,6 +55,45 @@ __device__ __forceinline__ void ms_st_sc1(double2* p, double2 v) {
                        __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store((mu64*)&p->y, (unsigned long long)__double_as_longlong(v.y), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// acc += pv(lane J of this lane's 16-lane row) * s, as c_fma (same order of the four products): v_fmac_f64 with its
+// first source taken by DPP row_newbcast, so a row value held once per row feeds the 16 lanes of the row. Every lane of
+// the wave must be active (the PT runs whole waves)
+template <int J>
+__device__ __forceinline__ void ms_cmac_bcast(double2& acc, const double2 pv, const double2 s) {
+    asm volatile(
+        "v_fmac_f64_dpp %0, %2, %4 row_newbcast:%c6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, -%3, %5 row_newbcast:%c6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %2, %5 row_newbcast:%c6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %3, %4 row_newbcast:%c6 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc.x), "+v"(acc.y)
+        : "v"(pv.x), "v"(pv.y), "v"(s.x), "v"(s.y), "i"(J));
+}
+// sum over j < KP of pv[j / 16](lane j % 16) * sreg[j]
+template <int J, int KP, int NPV, int NS>
+__device__ __forceinline__ void ms_pt_bcast(double2& acc, const double2 (&pv)[NPV], const double2 (&sreg)[NS]) {
+    if constexpr (J < KP) {
+        ms_cmac_bcast<J % 16>(acc, pv[J / 16], sreg[J]);
+        ms_pt_bcast<J + 1, KP>(acc, pv, sreg);
+    }
+}
+// a DPP source must not be written by a VALU instruction in the two cycles before it (the row values come from LDS
+// reads; this keeps two wait states after whatever the compiler puts between them and the products)
+template <int NPV>
+__device__ __forceinline__ void ms_nop_for(const double2 (&pv)[NPV]) {
+#pragma unroll
+    for (int c = 0; c < NPV; ++c) asm volatile("" ::"v"(pv[c].x), "v"(pv[c].y));
+    asm volatile("s_nop 1");
+}
+
+// plain 16-B global store: the line stays in the XCD's L2 (an sc1 store drops it, and the same-XCD readers then fetch
+// it at the cross-XCD rate, MI355X_MICROARCH.md § visibility, store flavours). Used only where every workgroup of the
+// group runs on one XCD (checked at the first poll: see l2keep)
+__device__ __forceinline__ void ms_st_keep(double2* p, double2 v) {
+    typedef double v2f64 __attribute__((ext_vector_type(2)));
+    v2f64 w = {v.x, v.y};
+    *(__attribute__((address_space(1))) v2f64*)p = w;
 }
 
 // plain global load (global_load, not flat_load: a flat load also counts in lgkmcnt)
@@ -78,6 +120,7 @@ struct MsLayout {
     static constexpr int EPT = (N2 + RG - 1) / RG;  // state rows per thread and trajectory in the gather
     static constexpr int GCH = CHI > 64 ? 1 : (R >= 4 ? 2 : (EPT <= 4 ? 4 : 1));  // trajectories per half with gather loads in flight
     static constexpr int PRB = (R >= 4 || CHI > 64) ? 4 : KPER;  // row values in flight in the PT (R = 4: 128 registers per thread)
+    static constexpr int PVR = (KPER + 15) / 16;   // registers of 16 row values (DPP row broadcast in the PT)
     static constexpr int TBMAX = CHI > 64 ? 8 : (R == 1 ? 32 : (R == 2 ? 16 : 8));
     static constexpr int TBC = R >= 4 ? 4 : 8;      // trajectories per PT pass (LDS partials)
     static constexpr int OMAX = 8;                  // outputs per trajectory
@@ -96,8 +139,8 @@ struct MsLayout {
 };
 
 // diagnostics (PQD_ABLATE bit 64, scripts/msplit_stamps.py): s_memtime at the phase boundaries of steps 1000..1015 in
-// workgroups 0 and 1 of group 0 (thread 0): [wg][step][phase 0..7]
-__device__ unsigned long long g_ms_stamps[2 * 16 * 8];
+// workgroups 0 and 1 of group 0 (thread 0): [wg][step][slot 0..31]
+__device__ unsigned long long g_ms_stamps[2 * 16 * 32];
 
 template <int N2, int CHI, int R, bool STAMP = false>
 __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, MsplitParams q,
@@ -106,7 +149,8 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
     using L = MsLayout<N2, CHI, R>;
     constexpr int NT = L::NT, HT = L::HT, KG = L::KG, KPER = L::KPER, RG = L::RG, EPT = L::EPT, NW = L::NW;
     constexpr int G = L::G, E = N2 * CHI, m2 = N2 * N2, TBM = L::TBMAX;
-    static_assert(L::LDS <= 160 * 1024, "LDS budget");
+    static_assert(L::LDS + 4 + 32 * L::TBMAX + 4 * MS_CEV_MAX + 8 * (L::FPT + L::WPT) * L::NT <= 160 * 1024,
+                  "LDS budget (dynamic + static)");
     static_assert(KPER * KG == CHI && CHI / RG == KPER, "gather columns = the k-group's slice rows");
     extern __shared__ __attribute__((aligned(16))) double2 smem[];
     __shared__ int s_abort;
@@ -117,7 +161,7 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
     __shared__ long long s_wo[TBM];
 
     const int tid = threadIdx.x, lane = tid & 63;
-    const int h = tid / HT, ht = tid - h * HT;  // half, thread within the half
+    const int h = R == 1 ? 0 : __builtin_amdgcn_readfirstlane(tid / HT), ht = tid - h * HT;  // half (wave-uniform), thread in it
     int grp, g;
     if (q.xcd > 0) {
         // XCD-grouped grid: block b sits in XCD slot b % 8 under the observed round-robin dealing; slot xs holds the
@@ -133,11 +177,19 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
     const int TB = q.TB, n_out = p.n_out;
     const int n_end = q.gend[grp];
     // phase stamps: 0 top, 1 PT partials (barrier), 2 published + arrived, 3 operands staged, 4 peers arrived (poll +
-    // barrier), 5 gather loads and operand loads issued, 6 gather done, 7 end barrier
+    // barrier), 5 gather loads and operand loads issued, 6 first chunk's loads returned, 7 gather done, 8 end barrier;
+    // per wave w < 8: 16 + w first chunk's loads returned, 24 + w gather done
     auto stamp = [&](int n, int k) {
         if constexpr (STAMP) {
             if (grp == 0 && g < 2 && threadIdx.x == 0 && n >= 1000 && n < 1016)
-                g_ms_stamps[(g * 16 + (n - 1000)) * 8 + k] = __builtin_amdgcn_s_memtime();
+                g_ms_stamps[(g * 16 + (n - 1000)) * 32 + k] = __builtin_amdgcn_s_memtime();
+        }
+    };
+    // per wave (lane 0 of waves 0..7): slot base + wave
+    auto wstamp = [&](int n, int base) {
+        if constexpr (STAMP) {
+            if (grp == 0 && g < 2 && lane == 0 && tid < 8 * 64 && n >= 1000 && n < 1016)
+                g_ms_stamps[(g * 16 + (n - 1000)) * 32 + base + (tid >> 6)] = __builtin_amdgcn_s_memtime();
         }
     };
     const int alpha = R * g + h;          // this half's PT row
@@ -158,11 +210,21 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
     double2* __restrict__ Xg = X + (size_t)grp * TB * 2 * E;
     const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(Xg, 0, TB * 2 * E * 16, 0x00020000);
     unsigned* ct = cnt + (size_t)grp * 64;
+    // l2keep (XCD-grouped grid): payload stores keep their lines in the XCD's L2, which is coherent for the readers'
+    // sc1 loads only if every workgroup of the group runs on that XCD. Each arrival word carries its writer's XCD id
+    // (bits 28..30, HW_REG_XCC_ID) and the first poll checks them; a group spread over XCDs ends the launch before its
+    // first gather (error words 0 and 1) and the host re-runs it with sc1 stores. PQD_ABLATE bit 512 fakes a spread
+    // group (workgroup 0 reports the next XCD) for the test of that path.
+    unsigned xtag = 0;
+    if (q.l2keep) {
+        unsigned xid = (unsigned)__builtin_amdgcn_s_getreg(MS_HWREG_XCC_ID) & 7u;
+        if ((p.ablate & 512) && g == 0) xid = (xid + 1u) & 7u;
+        xtag = xid << 28;
+    }
 
     // thread roles in its half: PT (kq, j): slice rows kq KPER + jj, column j; gather (kq, c = j / RG, rg = j % RG):
     // column kcol = kq KPER + c of rows rg + RG i
-    const int kq = ht / CHI, j = ht - kq * CHI, cgi = j / RG, rg = j - cgi * RG;
-    const int kcol = kq * KPER + cgi;
+    const int kq = ht / CHI, j = ht - kq * CHI;
     const int grow = live ? p.gmap[alpha] : 0;
     double2 sreg[KPER];
     auto fetch_slice = [&](int si) {
@@ -235,9 +297,16 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
     // W(m) are the stored operators.
     // cursors: ci = position in s_cev, ce = its end, cg = global composite index - position, cs = s_cev[ci] or INT_MAX
     const double2* fbase[L::FPT];
-    int f_row[L::FPT], f_we[L::FPT], f_cs[L::FPT], f_ci[L::FPT], f_ce[L::FPT], f_cg[L::FPT];
+    // the rarely used cursor fields (position, end, global offset, row) live in LDS, one slot per thread and entry:
+    // in registers they pushed the gather past the VGPR budget, and the spill reloads' vmcnt waits sat among the
+    // gather's loads
+    // packed: [0] = position | end << 10 | row << 20 (positions <= MS_CEV_MAX, rows < N2 * N2 or n_out * N2), [1] =
+    // global composite index - position
+    static_assert(MS_CEV_MAX < 1024 && N2 * N2 < 2048 && L::OMAX * N2 < 2048, "cursor packing");
+    __shared__ int s_fcur[2][L::FPT * NT], s_wcur[2][L::WPT * NT];
+    int f_we[L::FPT], f_cs[L::FPT];
     const double2* wbase[L::WPT];
-    int w_rr[L::WPT], w_wb[L::WPT], w_we[L::WPT], w_cs[L::WPT], w_ci[L::WPT], w_ce[L::WPT], w_cg[L::WPT];
+    int w_wb[L::WPT], w_we[L::WPT], w_cs[L::WPT];
     auto first_comp = [&](int b, int from, int& cs, int& ci, int& ce, int& cg) {
         int i = s_cvo[b];
         ce = i + s_eve[b] - s_evi[b];
@@ -251,10 +320,12 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
         const int e = tid + NT * i;
         const bool in = e < R * TB * N2;
         const int r = in ? e / (TB * N2) : 0, b = in ? (e / N2) % TB : 0, be = e % N2, a = R * g + r;
-        f_row[i] = a * N2 + be;
-        fbase[i] = p.F + (size_t)s_sy[b] * p.f_stride + f_row[i];
+        fbase[i] = p.F + (size_t)s_sy[b] * p.f_stride + a * N2 + be;
         f_we[i] = (in && a < N2) ? s_we[b] : -1;
-        first_comp(b, 1, f_cs[i], f_ci[i], f_ce[i], f_cg[i]);
+        int ci, ce, cg;
+        first_comp(b, 1, f_cs[i], ci, ce, cg);
+        s_fcur[0][i * NT + tid] = ci | (ce << 10) | ((a * N2 + be) << 20);
+        s_fcur[1][i * NT + tid] = cg;
     }
 #pragma unroll
     for (int i = 0; i < L::WPT; ++i) {
@@ -262,11 +333,14 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
         const int mb = e / wrow, rr = e - mb * wrow;
         const bool in = mb < tmine;
         const int b = in ? g + G * mb : 0;
-        w_rr[i] = rr;
+
         wbase[i] = p.W + (size_t)s_sy[b] * p.w_stride + rr;
         w_wb[i] = in ? s_wb[b] : INT_MAX;
         w_we[i] = in ? s_we[b] : -1;
-        first_comp(b, 1, w_cs[i], w_ci[i], w_ce[i], w_cg[i]);
+        int ci, ce, cg;
+        first_comp(b, 1, w_cs[i], ci, ce, cg);
+        s_wcur[0][i * NT + tid] = ci | (ce << 10) | (rr << 20);
+        s_wcur[1][i * NT + tid] = cg;
     }
     // operands of step m into registers (staged into LDS one step later). Every lane issues the same number of loads
     // (entries it does not need read rho0[0]), so the gather's waits can leave them in flight.
@@ -279,12 +353,16 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
             if (m < f_we[i]) {
                 src = fbase[i] + (size_t)m * m2;
                 if (m >= f_cs[i]) {  // rare: a composite at m (cursor moved past composites before m)
-                    while (f_cs[i] < m) { ++f_ci[i]; f_cs[i] = f_ci[i] < f_ce[i] ? s_cev[f_ci[i]] : INT_MAX; }
+                    const int pk = s_fcur[0][i * NT + tid];
+                    int ci = pk & 1023;
+                    const int ce = (pk >> 10) & 1023;
+                    while (f_cs[i] < m) { ++ci; f_cs[i] = ci < ce ? s_cev[ci] : INT_MAX; }
                     if (f_cs[i] == m) {
-                        src = q.Fev + (size_t)(f_ci[i] + f_cg[i]) * m2 + f_row[i];
-                        ++f_ci[i];
-                        f_cs[i] = f_ci[i] < f_ce[i] ? s_cev[f_ci[i]] : INT_MAX;
+                        src = q.Fev + (size_t)(ci + s_fcur[1][i * NT + tid]) * m2 + (pk >> 20);
+                        ++ci;
+                        f_cs[i] = ci < ce ? s_cev[ci] : INT_MAX;
                     }
+                    s_fcur[0][i * NT + tid] = (pk & ~1023) | ci;
                 }
             }
             fpre[i] = ms_gld(src);
@@ -295,12 +373,16 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
             if (m >= w_wb[i] && m <= w_we[i]) {
                 src = wbase[i] + (size_t)m * wrow;
                 if (m >= w_cs[i]) {
-                    while (w_cs[i] < m) { ++w_ci[i]; w_cs[i] = w_ci[i] < w_ce[i] ? s_cev[w_ci[i]] : INT_MAX; }
+                    const int pk = s_wcur[0][i * NT + tid];
+                    int ci = pk & 1023;
+                    const int ce = (pk >> 10) & 1023;
+                    while (w_cs[i] < m) { ++ci; w_cs[i] = ci < ce ? s_cev[ci] : INT_MAX; }
                     if (w_cs[i] == m) {
-                        src = q.Wev + (size_t)(w_ci[i] + w_cg[i]) * wrow + w_rr[i];
-                        ++w_ci[i];
-                        w_cs[i] = w_ci[i] < w_ce[i] ? s_cev[w_ci[i]] : INT_MAX;
+                        src = q.Wev + (size_t)(ci + s_wcur[1][i * NT + tid]) * wrow + (pk >> 20);
+                        ++ci;
+                        w_cs[i] = ci < ce ? s_cev[ci] : INT_MAX;
                     }
+                    s_wcur[0][i * NT + tid] = (pk & ~1023) | ci;
                 }
             }
             wpre[i] = ms_gld(src);
@@ -355,13 +437,40 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
         // ---- PT(n), half h: row alpha_h of every trajectory that continues past n, TBC at a time (LDS partials)
         for (int b0 = 0; b0 < TB; b0 += L::TBC) {
             const int nb = TB - b0 < L::TBC ? TB - b0 : L::TBC;
-            if (live) {
+            bool bcast = true;
+            if constexpr (STAMP) bcast = !(p.ablate & 4096);
+            if (live && bcast) {
+                // lane i of each 16-lane row reads row value kq KPER + 16 c + i (one ds_read_b128 per 16 values, all
+                // rows of a wave share kq) and the products take it by DPP row_newbcast: the per-value broadcast
+                // reads were one 4-cycle LDS instruction per complex MAC per wave. The row values of PF trajectories
+                // are read at once (one exposed LDS latency per PF trajectories)
+                constexpr int PF = CHI <= 32 ? L::TBC : (CHI <= 64 ? 4 : 1);
+                for (int bq = 0; bq < nb; bq += PF) {
+                    double2 pv[PF][L::PVR];
+#pragma unroll
+                    for (int u = 0; u < PF; ++u)
+#pragma unroll
+                        for (int c = 0; c < L::PVR; ++c) {
+                            const int jv = 16 * c + (lane & 15);
+                            pv[u][c] = smem[L::PRO + (h * TBM + b0 + bq + u) * CHI + kq * KPER + (jv < KPER ? jv : KPER - 1)];
+                        }
+#pragma unroll
+                    for (int u = 0; u < PF; ++u) {
+                        const int bb = bq + u, b = b0 + bb;
+                        if (bb >= nb || !((act >> b) & 1)) continue;
+                        double2 acc = c_zero();
+                        ms_nop_for(pv[u]);
+                        ms_pt_bcast<0, KPER>(acc, pv[u], sreg);
+                        smem[L::REDO + (h * L::TBC + bb) * HT + ht] = acc;
+                    }
+                }
+            } else if (live) {
                 for (int bb = 0; bb < nb; ++bb) {
                     const int b = b0 + bb;
                     if (!((act >> b) & 1)) continue;
+                    double2 acc = c_zero();
                     // every row value in flight before the first product (one at a time, the broadcast LDS reads
                     // were a chain of round trips: ≈1,600 cycles for 16 complex MACs, scripts/msplit_stamps.py)
-                    double2 acc = c_zero();
 #pragma unroll
                     for (int j0 = 0; j0 < KPER; j0 += L::PRB) {
                         double2 prv[L::PRB];
@@ -383,7 +492,8 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
                     double2 y = smem[L::REDO + (h * L::TBC + bb) * HT + d];
 #pragma unroll
                     for (int k2 = 1; k2 < KG; ++k2) y = c_add(y, smem[L::REDO + (h * L::TBC + bb) * HT + k2 * CHI + d]);
-                    ms_st_sc1(Xg + ((size_t)b * 2 + (n & 1)) * E + (size_t)alpha * CHI + d, y);
+                    double2* dst = Xg + ((size_t)b * 2 + (n & 1)) * E + (size_t)alpha * CHI + d;
+                    if (q.l2keep) ms_st_keep(dst, y); else ms_st_sc1(dst, y);
                 }
             }
             if (b0 + L::TBC < TB) __syncthreads();  // REDO reused by the next pass
@@ -393,7 +503,7 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) __hip_atomic_store((mu32*)(ct + g), (unsigned)n + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) __hip_atomic_store((mu32*)(ct + g), ((unsigned)n + 1u) | xtag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         stamp(n, 2);
         // ---- operands of step n + 1 (loaded during step n - 1's gather) to LDS
         stage_ops();
@@ -423,16 +533,26 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
             const unsigned want = (unsigned)n + 1u;
             unsigned spins = 0;
             bool ok = true;
+            bool placed = true;
             for (;;) {
                 const unsigned v =
                     lane < G ? __hip_atomic_load((mu32*)(ct + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : want;
-                if (__all(v >= want)) break;
+                if (__all((v & MS_STEP_MASK) >= want)) {
+                    // first poll: every peer's XCD id is in its word; the same words reach every workgroup of the group,
+                    // so all of them take the same decision
+                    if (q.l2keep && n == 0) {
+                        const unsigned x0 = __builtin_amdgcn_readfirstlane(v) >> 28;
+                        placed = __all(lane >= G || (v >> 28) == x0);
+                    }
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(1);
                 if (++spins > p.spin_limit) { ok = false; break; }
             }
             if (tid == 0) {
-                s_abort = ok ? 0 : 1;
-                if (!ok) __hip_atomic_store((mu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_abort = ok && placed ? 0 : 1;
+                if (!placed) __hip_atomic_store((mu32*)(err + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (s_abort) __hip_atomic_store((mu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         __syncthreads();
@@ -443,6 +563,13 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
         // of this workgroup's trajectories
         // the first chunk is peeled (first = true: the operand loads are issued behind its gather loads); a loop body
         // shared by chunks with and without those loads would wait for the gather with the smaller count
+        // the gather's thread roles recomputed from an opaque copy of the thread index each step: derived from the
+        // launch-time values, the compiler kept a dozen precomputed LDS addresses alive across the loop, spilled
+        // them, and each reload's vmcnt wait held the gather behind the operand and slice loads
+        int tg = tid;
+        asm volatile("" : "+v"(tg));
+        const int gj = (tg & (HT - 1)) & (CHI - 1), gcg = gj / RG;
+        const int rg = gj - gcg * RG, kcol = ((tg & (HT - 1)) / CHI) * KPER + gcg;
         const double2 cv = smem[L::CLO + kcol];
         auto chunk = [&](auto gct, auto firstt, int b0) {
             constexpr int GC = decltype(gct)::value;
@@ -451,15 +578,21 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
             // whole wave): loads that are consumed on some paths only stay pending in the waitcnt pass across the loops,
             // and the waits it then puts in front of the next chunk's loads serialised the chunk's round trips
             v4u32m xr[GC][EPT];
+            // timing-only variants (STAMP builds): 2048 rotates the chunk's trajectory order by the workgroup index,
+            // 1024 points every gather load at element 0 (results not used)
+            int rot = 0;
+            if constexpr (STAMP) rot = (p.ablate & 2048) ? g : 0;
+            auto slot_b = [&](int bb) { return b0 + R * (GC > 1 ? (bb + rot) % GC : bb); };
 #pragma unroll
             for (int bb = 0; bb < GC; ++bb) {
-                const int b = b0 + R * bb;
+                const int b = slot_b(bb);
                 const bool on = b < TB && ((act >> b) & 1);
 #pragma unroll
                 for (int i = 0; i < EPT; ++i) {
                     const int be = rg + RG * i;
-                    const int off = on ? (int)((((size_t)b * 2 + (n & 1)) * E + (size_t)(be < N2 ? be : 0) * CHI + kcol) * 16)
-                                       : 0;
+                    int off = on ? (int)((((size_t)b * 2 + (n & 1)) * E + (size_t)(be < N2 ? be : 0) * CHI + kcol) * 16)
+                                 : 0;
+                    if constexpr (STAMP) off = (p.ablate & 1024) ? 0 : off;
                     xr[bb][i] = __builtin_amdgcn_raw_buffer_load_b128(rX, off, 0, 16);
                 }
             }
@@ -473,23 +606,32 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
             for (int bb = 0; bb < GC; ++bb)
 #pragma unroll
                 for (int i = 0; i < EPT; ++i) asm volatile("" ::"v"(xr[bb][i]));
+            if constexpr (FIRST) { stamp(n, 6); wstamp(n, 16); }
 #pragma unroll
             for (int bb = 0; bb < GC; ++bb) {
-                const int b = b0 + R * bb;
+                const int b = slot_b(bb);
                 if (b >= TB || !((act >> b) & 1)) continue;
                 double2 xv[EPT];
 #pragma unroll
                 for (int i = 0; i < EPT; ++i)
                     xv[i] = make_double2(__hiloint2double((int)xr[bb][i].y, (int)xr[bb][i].x),
                                          __hiloint2double((int)xr[bb][i].w, (int)xr[bb][i].z));
+                // the operand entries of a row are read from LDS together and then used (read one by one next to
+                // their products, each read's latency was exposed: ≈9,300 cycles for 8 trajectories' rows)
                 if ((nxt >> b) & 1) {
 #pragma unroll
                     for (int r = 0; r < R; ++r) {
                         if (R * g + r >= N2) continue;
+                        double2 fv[EPT];
+#pragma unroll
+                        for (int i = 0; i < EPT; ++i) {
+                            const int be = rg + RG * i;
+                            fv[i] = smem[L::FRO + (r * TBM + b) * N2 + (be < N2 ? be : 0)];
+                        }
                         double2 part = c_zero();
 #pragma unroll
                         for (int i = 0; i < EPT; ++i)
-                            if (rg + RG * i < N2) c_fma(part, smem[L::FRO + (r * TBM + b) * N2 + rg + RG * i], xv[i]);
+                            if (rg + RG * i < N2) c_fma(part, fv[i], xv[i]);
                         part = c_group_sum<4>(part);
                         if (rg == 0) smem[L::PRO + (r * TBM + b) * CHI + kcol] = part;
                     }
@@ -499,10 +641,16 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
                     // is left to flush (next step, while wave 0 polls)
                     const int mb = b / G;
                     for (int k = 0; k < n_out; ++k) {
+                        double2 wv[EPT];
+#pragma unroll
+                        for (int i = 0; i < EPT; ++i) {
+                            const int be = rg + RG * i;
+                            wv[i] = smem[L::WLO + (mb * L::OMAX + k) * N2 + (be < N2 ? be : 0)];
+                        }
                         double2 o = c_zero();
 #pragma unroll
                         for (int i = 0; i < EPT; ++i)
-                            if (rg + RG * i < N2) c_fma(o, smem[L::WLO + (mb * L::OMAX + k) * N2 + rg + RG * i], xv[i]);
+                            if (rg + RG * i < N2) c_fma(o, wv[i], xv[i]);
                         o = c_group_sum<4>(o);
                         if (rg == 0) smem[L::OPO + (mb * L::OMAX + k) * CHI + kcol] = c_mul(o, cv);
                     }
@@ -519,9 +667,10 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
         if (fc == 0 && nh >= 1) { chunk(MsIC<1>{}, MsIC<1>{}, h); fc = 1; }
         if (fc == 0) issue_ops();
         for (int b0 = h + R * fc; b0 < TB; b0 += R * L::GCH) chunk(MsIC<L::GCH>{}, MsIC<0>{}, b0);
-        stamp(n, 6);
-        __syncthreads();  // r_b from every half before PT(m)
         stamp(n, 7);
+        wstamp(n, 24);
+        __syncthreads();  // r_b from every half before PT(m)
+        stamp(n, 8);
     }
 }
 
@@ -699,7 +848,7 @@ hipError_t launch_msplit(int N2, int CHI, const SweepParams& p, const MsplitPara
     }
 }
 
-// diagnostics: the stamps of the last PQD_ABLATE=64 multi-trajectory split launch (2 workgroups x 16 steps x 8 phases)
+// diagnostics: the stamps of the last PQD_ABLATE=64 multi-trajectory split launch (2 workgroups x 16 steps x 32 slots)
 extern "C" int pqd_debug_msplit_stamps(unsigned long long* out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ms_stamps), sizeof(unsigned long long) * 256) == hipSuccess ? 0 : 4;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ms_stamps), sizeof(unsigned long long) * 1024) == hipSuccess ? 0 : 4;
 }

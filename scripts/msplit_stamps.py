@@ -2,8 +2,9 @@
 
 A diagnostic instantiation (PQD_ABLATE bit 64; N2 = 16, chi = 64) records s_memtime in workgroups 0 and 1 of group 0
 (thread 0) at the phase boundaries of steps 1000..1015; this prints the mean shader cycles of each phase:
-  0 top -> 1 PT partials + barrier -> 2 published (sc1 stores, drain, barrier, arrival word) -> 3 operands staged to
-  LDS -> 4 peers arrived (poll + barrier) -> 5 gather loads + operand loads issued -> 6 gather done -> 7 end barrier
+  0 top -> 1 PT partials + barrier -> 2 published (stores, drain, barrier, arrival word) -> 3 operands staged to
+  LDS -> 4 peers arrived (poll + barrier) -> 5 gather loads + operand loads issued -> 6 the first chunk's loads back
+  -> 7 gather done -> 8 end barrier; and per wave when the first chunk's loads are back and the gather is done
 usage: python scripts/msplit_stamps.py [--n-t1 32] [--n-tau 2000]   (the C4 sweep shape, bench.build_workload)
 """
 import argparse
@@ -16,15 +17,15 @@ import numpy as np
 HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, HERE)
 
-NAMES = ["PT + barrier", "publish+arrive", "stage operands", "poll peers", "gather issue", "gather compute",
-         "end barrier"]
+NAMES = ["PT + barrier", "publish+arrive", "stage operands", "poll peers", "gather issue", "gather loads back",
+         "gather compute", "end barrier"]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n-t1", type=int, default=32)
     ap.add_argument("--n-tau", type=int, default=2000)
-    ap.add_argument("--ablate", type=int, default=0, help="extra PQD_ABLATE bits (timing only: 128 no operand loads)")
+    ap.add_argument("--ablate", type=int, default=0, help="extra PQD_ABLATE bits (timing only: 128 no operand loads, 1024 gather loads at element 0, 2048 per-workgroup rotation of the gather order)")
     args = ap.parse_args()
     import bench
     from pyaceqd_amd import _lib, engine
@@ -40,20 +41,22 @@ def main():
     plan.synchronize()
     _, ms, _ = plan.timing(reset=True)
     print(f"sweep {ms:.2f} ms, {ms * 1e3 / (grid.n_steps + 1):.3f} us per step")
-    buf = (C.c_ulonglong * 256)()
+    buf = (C.c_ulonglong * 1024)()
     fn = _lib.lib().pqd_debug_msplit_stamps
     fn.argtypes = [C.c_void_p]
     assert fn(buf) == 0
-    st = np.array(buf[:256], dtype=np.int64).reshape(2, 16, 8)
+    st = np.array(buf[:1024], dtype=np.int64).reshape(2, 16, 32)
     for w in range(2):
-        s = st[w]
+        s = st[w, :, :9]
         ph = np.diff(s, axis=1)
         step = np.diff(s[:, 0])
         print(f"workgroup {w}: mean shader cycles per step {step.mean():.0f} (min {step.min()}, max {step.max()})")
         for k, nm in enumerate(NAMES):
             print(f"  {nm:16s} {ph[:, k].mean():8.0f}   min {ph[:, k].min():6d}  max {ph[:, k].max():6d}")
         print(f"  {'(end -> next 0)':16s} {(s[1:, 0] - s[:-1, -1]).mean():8.0f}")
-
+        for nm, b in (("loads back", 16), ("gather done", 24)):
+            d = st[w, :, b:b + 8] - st[w, :, 4:5]  # cycles after the poll, waves 0..7
+            print(f"  {nm} after the poll, waves 0..7:", " ".join(f"{v:.0f}" for v in d.mean(axis=0)))
 
 if __name__ == "__main__":
     main()

@@ -173,3 +173,44 @@ def test_msplit_repeated_executes_and_rebuild(monkeypatch):
     for x, y, z in zip(a, b, c):
         np.testing.assert_array_equal(x, y)
         np.testing.assert_array_equal(x, z)
+
+
+@pytest.mark.parametrize("l2", ["1", "0"])
+def test_msplit_exchange_store_flavours(monkeypatch, l2):
+    """XCD-grouped grid: exchange stores that keep their L2 lines (default, the group's placement on one XCD checked
+    at its first poll) and sc1 stores (PQD_MS_L2=0); both vs the oracle, no fallback"""
+    monkeypatch.setenv("PQD_MSPLIT", "2")
+    monkeypatch.setenv("PQD_MS_L2", l2)
+    N, chi = 4, 64
+    sysd, grid = H.random_system(N, n_steps=40, seed=21)
+    tr = mixed_trajectories(40, N, 48, seed=12)
+    pt = ptmod.random_pt(N, chi, D=16, n_slices=7, seed=4, eps=0.12)
+    ops = [H.ketbra(N, 1, 1), H.ketbra(N, 2, 0)]
+    rho0 = H.random_rho(N)
+    plan = engine.Plan(sysd, grid, rho0, ops, tr, pt=pt)
+    plan.execute()
+    got = plan.download()
+    assert plan.info()[0] == MSPLIT and plan.info()[2] == 0
+    cmp_lists(got, oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
+
+
+def test_msplit_spread_group_reruns_with_sc1_stores(monkeypatch):
+    """PQD_ABLATE=512: workgroup 0 of every group reports another XCD, so the first poll finds the group spread; the
+    launch ends before its first gather and the plan re-runs it with sc1 exchange stores (one fallback, still on split
+    groups), vs the oracle"""
+    monkeypatch.setenv("PQD_MSPLIT", "2")
+    monkeypatch.setenv("PQD_ABLATE", "512")
+    N, chi = 4, 64
+    sysd, grid = H.random_system(N, n_steps=30, seed=22)
+    tr = mixed_trajectories(30, N, 40, seed=13)
+    pt = ptmod.random_pt(N, chi, D=16, n_slices=6, seed=5, eps=0.1)
+    ops = [H.ketbra(N, 0, 0), H.ketbra(N, 3, 1)]
+    rho0 = H.random_rho(N)
+    plan = engine.Plan(sysd, grid, rho0, ops, tr, pt=pt)
+    plan.execute()
+    got = plan.download()
+    assert plan.info()[0] == MSPLIT and plan.info()[2] == 1
+    cmp_lists(got, oracle.propagate(sysd, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
+    plan.execute()  # stays on sc1 stores: no further fallback
+    cmp_lists(plan.download(), got, 1e-15)
+    assert plan.info()[2] == 1
