@@ -19,8 +19,9 @@
 //   poll      wave 0 reads the G arrival words of the group (one relaxed sc1 load per poll), the others wait at a barrier
 //   gather    half h takes the trajectories b = h, h + R, ...: every element of each state by 16-B sc1 buffer loads,
 //             up to 4 trajectories' loads in flight per thread; thread (kq, c, rg) takes column kq KPER + c of rows
-//             rg + 4 i and contracts them with F_b(n + 1)[alpha][.] for all R rows of the workgroup (each element is
-//             loaded once per workgroup), the 4 row groups summed by DPP (quad_perm); one barrier, then PT(n + 1)
+//             rg + 4 i (consecutive lanes consecutive columns) and contracts them with F_b(n + 1)[alpha][.] for all R
+//             rows of the workgroup (each element is loaded once per workgroup), the 4 row groups summed by permlane
+//             swaps; one barrier, then PT(n + 1)
 //   outputs   trajectory b's outputs are written by workgroup b mod G (the half that gathers b) from the state it
 //             loads anyway: <O_k>(n + 1) = sum W_b(n + 1)[k][beta] Q_b[beta][d] c[d], one wave sum each, the wave
 //             partials added after the next PT barrier — no output workgroup
@@ -85,6 +86,19 @@ __device__ __forceinline__ void ms_nop_for(const double2 (&pv)[NPV]) {
 #pragma unroll
     for (int c = 0; c < NPV; ++c) asm volatile("" ::"v"(pv[c].x), "v"(pv[c].y));
     asm volatile("s_nop 1");
+}
+
+// sum over the 4 row groups of a gather column (lanes 8 / 16 apart at KPER = 8, 16 / 32 apart otherwise), left in all
+// four lanes with the same bits (each step adds the same pair: row_ror:8 inside a 16-lane row, then permlane swaps)
+template <int KP>
+__device__ __forceinline__ double2 ms_rg_sum(double2 v) {
+    if constexpr (KP == 8) {
+        v = c_add(v, make_double2(dpp_d<0x128>(v.x), dpp_d<0x128>(v.y)));
+        return make_double2(xor_add<16>(v.x), xor_add<16>(v.y));
+    } else {
+        v = make_double2(xor_add<16>(v.x), xor_add<16>(v.y));
+        return make_double2(xor_add<32>(v.x), xor_add<32>(v.y));
+    }
 }
 
 // plain 16-B global store: the line stays in the XCD's L2 (an sc1 store drops it, and the same-XCD readers then fetch
@@ -566,10 +580,23 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
         // the gather's thread roles recomputed from an opaque copy of the thread index each step: derived from the
         // launch-time values, the compiler kept a dozen precomputed LDS addresses alive across the loop, spilled
         // them, and each reload's vmcnt wait held the gather behind the operand and slice loads
+        // Lanes: 16 (KPER = 8: 8) consecutive lanes take consecutive columns of one row, so a wave's 16-B load is
+        // four (eight) contiguous 256-B (128-B) runs; with the row group in the low lane bits every lane was its own
+        // request, 16 B per cycle per CU instead of 51.6 (scripts/ubench/gather_bw.hip)
         int tg = tid;
         asm volatile("" : "+v"(tg));
-        const int gj = (tg & (HT - 1)) & (CHI - 1), gcg = gj / RG;
-        const int rg = gj - gcg * RG, kcol = ((tg & (HT - 1)) / CHI) * KPER + gcg;
+        const int gw = (tg & (HT - 1)) >> 6, gl = tg & 63;
+        int rg, kcol;
+        if constexpr (KPER == 8) {
+            rg = (gl >> 3) & 3;
+            kcol = (2 * gw + (gl >> 5)) * KPER + (gl & 7);
+        } else if constexpr (KPER == 16) {
+            rg = gl >> 4;
+            kcol = gw * KPER + (gl & 15);
+        } else {
+            rg = gl >> 4;
+            kcol = (gw >> 1) * KPER + 16 * (gw & 1) + (gl & 15);
+        }
         const double2 cv = smem[L::CLO + kcol];
         auto chunk = [&](auto gct, auto firstt, int b0) {
             constexpr int GC = decltype(gct)::value;
@@ -579,7 +606,7 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
             // and the waits it then puts in front of the next chunk's loads serialised the chunk's round trips
             v4u32m xr[GC][EPT];
             // timing-only variants (STAMP builds): 2048 rotates the chunk's trajectory order by the workgroup index,
-            // 1024 points every gather load at element 0 (results not used)
+            // 1024 points every gather load at element 0, 8192 those of half 1 (results not used)
             int rot = 0;
             if constexpr (STAMP) rot = (p.ablate & 2048) ? g : 0;
             auto slot_b = [&](int bb) { return b0 + R * (GC > 1 ? (bb + rot) % GC : bb); };
@@ -592,7 +619,7 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
                     const int be = rg + RG * i;
                     int off = on ? (int)((((size_t)b * 2 + (n & 1)) * E + (size_t)(be < N2 ? be : 0) * CHI + kcol) * 16)
                                  : 0;
-                    if constexpr (STAMP) off = (p.ablate & 1024) ? 0 : off;
+                    if constexpr (STAMP) off = ((p.ablate & 1024) || ((p.ablate & 8192) && h == 1)) ? 0 : off;
                     xr[bb][i] = __builtin_amdgcn_raw_buffer_load_b128(rX, off, 0, 16);
                 }
             }
@@ -632,7 +659,7 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
 #pragma unroll
                         for (int i = 0; i < EPT; ++i)
                             if (rg + RG * i < N2) c_fma(part, fv[i], xv[i]);
-                        part = c_group_sum<4>(part);
+                        part = ms_rg_sum<KPER>(part);
                         if (rg == 0) smem[L::PRO + (r * TBM + b) * CHI + kcol] = part;
                     }
                 }
@@ -651,7 +678,7 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
 #pragma unroll
                         for (int i = 0; i < EPT; ++i)
                             if (rg + RG * i < N2) c_fma(o, wv[i], xv[i]);
-                        o = c_group_sum<4>(o);
+                        o = ms_rg_sum<KPER>(o);
                         if (rg == 0) smem[L::OPO + (mb * L::OMAX + k) * CHI + kcol] = c_mul(o, cv);
                     }
                 }
