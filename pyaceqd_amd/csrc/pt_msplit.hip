@@ -9,10 +9,11 @@
 //
 // A workgroup is R "halves" of HT = 4 CHI threads; half h owns row alpha_h = R g + h. Per step n:
 //   PT(n)     half h: y_b = r_b^h . S_alpha_h(n) for every active trajectory b, r_b^h = row alpha_h of F_b(n) Q_b
-//             (from the gather of step n - 1): thread (kq, d) holds S[kq KPER + j][d] (j < KPER) in registers, the 4
-//             k-group partial sums meet in LDS
-//   publish   y_b -> exchange slot n & 1 of trajectory b (8-B sc1 relaxed atomic stores), every storing wave drains
-//             (s_waitcnt vmcnt(0)), a barrier, then ONE lane stores the workgroup's arrival word (= n + 1)
+//             (from the gather of step n - 1): thread (kq, d) holds S[kq KPER + j][d] (j < KPER) in registers; a
+//             wave's four 16-lane rows are the four k-groups of 16 columns, summed by permlane swaps
+//   publish   y_b -> exchange slot n & 1 of trajectory b (16-B stores that keep the line in the group's L2, or 8-B
+//             sc1 relaxed atomic stores: l2keep), every storing wave drains (s_waitcnt vmcnt(0)), a barrier, then ONE
+//             lane stores the workgroup's arrival word (= n + 1, with its XCD id)
 //   operands  F_b(n + 1) rows and the output rows W_b(n + 1) were loaded into registers during step n - 1: they go to
 //             LDS now and the loads of step n + 2's are issued (an operand load never sits between a publish and a
 //             poll); then the next slice rows when the schedule changes them
@@ -133,17 +134,14 @@ struct MsLayout {
     static constexpr int RG = 4;                    // gather row groups: lanes 4 c + rg of a k-group
     static constexpr int EPT = (N2 + RG - 1) / RG;  // state rows per thread and trajectory in the gather
     static constexpr int GCH = CHI > 64 ? 1 : (R >= 4 ? 2 : (EPT <= 4 ? 4 : 1));  // trajectories per half with gather loads in flight
-    static constexpr int PRB = (R >= 4 || CHI > 64) ? 4 : KPER;  // row values in flight in the PT (R = 4: 128 registers per thread)
     static constexpr int PVR = (KPER + 15) / 16;   // registers of 16 row values (DPP row broadcast in the PT)
     static constexpr int TBMAX = CHI > 64 ? 8 : (R == 1 ? 32 : (R == 2 ? 16 : 8));
-    static constexpr int TBC = R >= 4 ? 4 : 8;      // trajectories per PT pass (LDS partials)
     static constexpr int OMAX = 8;                  // outputs per trajectory
     static constexpr int TMINE = (TBMAX + G - 1) / G;  // trajectories whose outputs one workgroup writes
     static constexpr int FPT = (R * TBMAX * N2 + NT - 1) / NT;      // F-row entries per thread
     static constexpr int WPT = (TMINE * OMAX * N2 + NT - 1) / NT;   // output-row entries per thread
     static constexpr int PRO = 0;                        // r_b rows [R][TBMAX][CHI]
-    static constexpr int REDO = PRO + R * TBMAX * CHI;   // PT partials [R][TBC][HT]
-    static constexpr int FRO = REDO + R * TBC * HT;      // F_b(n + 1) rows of the workgroup [R][TBMAX][N2]
+    static constexpr int FRO = PRO + R * TBMAX * CHI;    // F_b(n + 1) rows of the workgroup [R][TBMAX][N2]
     static constexpr int WLO = FRO + R * TBMAX * N2;     // output rows [TMINE][OMAX][N2]
     static constexpr int CLO = WLO + TMINE * OMAX * N2;  // closure vector of the outputs the gather writes [CHI]
     static constexpr int OPO = CLO + CHI;                // output columns (W row x state, times the closure) [TMINE][OMAX][CHI]
@@ -236,9 +234,9 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
         xtag = xid << 28;
     }
 
-    // thread roles in its half: PT (kq, j): slice rows kq KPER + jj, column j; gather (kq, c = j / RG, rg = j % RG):
-    // column kcol = kq KPER + c of rows rg + RG i
-    const int kq = ht / CHI, j = ht - kq * CHI;
+    // thread roles in its half: PT (kq, j): slice rows kq KPER + jj of column j, kq = the lane's 16-lane row, j = 16
+    // (wave in the half) + lane % 16; the gather's roles are set in the step loop
+    const int kq = (ht & 63) >> 4, j = 16 * (ht >> 6) + (ht & 15);
     const int grow = live ? p.gmap[alpha] : 0;
     double2 sreg[KPER];
     auto fetch_slice = [&](int si) {
@@ -448,70 +446,39 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
         const unsigned long long act = mask(n < my_we);                      // PT(n), published, gathered
         const unsigned long long nxt = mask(m < my_we);                      // r_b for PT(m)
         const unsigned long long own = mask(lane < TB && lane % G == g && m >= my_wb && m <= my_we);  // outputs at m
-        // ---- PT(n), half h: row alpha_h of every trajectory that continues past n, TBC at a time (LDS partials)
-        for (int b0 = 0; b0 < TB; b0 += L::TBC) {
-            const int nb = TB - b0 < L::TBC ? TB - b0 : L::TBC;
-            bool bcast = true;
-            if constexpr (STAMP) bcast = !(p.ablate & 4096);
-            if (live && bcast) {
-                // lane i of each 16-lane row reads row value kq KPER + 16 c + i (one ds_read_b128 per 16 values, all
-                // rows of a wave share kq) and the products take it by DPP row_newbcast: the per-value broadcast
-                // reads were one 4-cycle LDS instruction per complex MAC per wave. The row values of PF trajectories
-                // are read at once (one exposed LDS latency per PF trajectories)
-                constexpr int PF = CHI <= 32 ? L::TBC : (CHI <= 64 ? 4 : 1);
-                for (int bq = 0; bq < nb; bq += PF) {
-                    double2 pv[PF][L::PVR];
+        // ---- PT(n), half h: row alpha_h of every trajectory that continues past n. Wave w of the half takes columns
+        // 16 w .. 16 w + 15 and its four 16-lane rows the four k-groups (KPER slice rows each): lane i of row kq reads
+        // row value kq KPER + 16 c + i (one ds_read_b128 per wave and 64 values), the products take it by DPP
+        // row_newbcast, two permlane swaps add the k-groups, and row 0 stores the 16 columns — no LDS partials and no
+        // barrier between the PT and the publish. The row values of PF trajectories are read at once
+        if (live) {
+            constexpr int PF = CHI <= 32 ? 8 : (CHI <= 64 ? 4 : 1);
+            for (int b0 = 0; b0 < TB; b0 += PF) {
+                double2 pv[PF][L::PVR];
 #pragma unroll
-                    for (int u = 0; u < PF; ++u)
+                for (int u = 0; u < PF; ++u)
 #pragma unroll
-                        for (int c = 0; c < L::PVR; ++c) {
-                            const int jv = 16 * c + (lane & 15);
-                            pv[u][c] = smem[L::PRO + (h * TBM + b0 + bq + u) * CHI + kq * KPER + (jv < KPER ? jv : KPER - 1)];
-                        }
-#pragma unroll
-                    for (int u = 0; u < PF; ++u) {
-                        const int bb = bq + u, b = b0 + bb;
-                        if (bb >= nb || !((act >> b) & 1)) continue;
-                        double2 acc = c_zero();
-                        ms_nop_for(pv[u]);
-                        ms_pt_bcast<0, KPER>(acc, pv[u], sreg);
-                        smem[L::REDO + (h * L::TBC + bb) * HT + ht] = acc;
+                    for (int c = 0; c < L::PVR; ++c) {
+                        const int jv = 16 * c + (lane & 15), bu = b0 + u < TBM ? b0 + u : TBM - 1;
+                        pv[u][c] = smem[L::PRO + (h * TBM + bu) * CHI + kq * KPER + (jv < KPER ? jv : KPER - 1)];
                     }
-                }
-            } else if (live) {
-                for (int bb = 0; bb < nb; ++bb) {
-                    const int b = b0 + bb;
-                    if (!((act >> b) & 1)) continue;
+#pragma unroll
+                for (int u = 0; u < PF; ++u) {
+                    const int b = b0 + u;
+                    if (b >= TB || !((act >> b) & 1)) continue;
                     double2 acc = c_zero();
-                    // every row value in flight before the first product (one at a time, the broadcast LDS reads
-                    // were a chain of round trips: ≈1,600 cycles for 16 complex MACs, scripts/msplit_stamps.py)
-#pragma unroll
-                    for (int j0 = 0; j0 < KPER; j0 += L::PRB) {
-                        double2 prv[L::PRB];
-#pragma unroll
-                        for (int jj = 0; jj < L::PRB; ++jj)
-                            prv[jj] = smem[L::PRO + (h * TBM + b) * CHI + kq * KPER + j0 + jj];
-#pragma unroll
-                        for (int jj = 0; jj < L::PRB; ++jj) c_fma(acc, prv[jj], sreg[j0 + jj]);
+                    ms_nop_for(pv[u]);
+                    ms_pt_bcast<0, KPER>(acc, pv[u], sreg);
+                    acc = make_double2(xor_add<16>(acc.x), xor_add<16>(acc.y));
+                    acc = make_double2(xor_add<32>(acc.x), xor_add<32>(acc.y));
+                    if (lane < 16) {
+                        double2* dst = Xg + ((size_t)b * 2 + (n & 1)) * E + (size_t)alpha * CHI + j;
+                        if (q.l2keep) ms_st_keep(dst, acc); else ms_st_sc1(dst, acc);
                     }
-                    smem[L::REDO + (h * L::TBC + bb) * HT + ht] = acc;
                 }
             }
-            __syncthreads();
-            if (b0 == 0) stamp(n, 1);
-            if (live) {
-                for (int e = ht; e < nb * CHI; e += HT) {
-                    const int bb = e / CHI, d = e - bb * CHI, b = b0 + bb;
-                    if (!((act >> b) & 1)) continue;
-                    double2 y = smem[L::REDO + (h * L::TBC + bb) * HT + d];
-#pragma unroll
-                    for (int k2 = 1; k2 < KG; ++k2) y = c_add(y, smem[L::REDO + (h * L::TBC + bb) * HT + k2 * CHI + d]);
-                    double2* dst = Xg + ((size_t)b * 2 + (n & 1)) * E + (size_t)alpha * CHI + d;
-                    if (q.l2keep) ms_st_keep(dst, y); else ms_st_sc1(dst, y);
-                }
-            }
-            if (b0 + L::TBC < TB) __syncthreads();  // REDO reused by the next pass
         }
+        stamp(n, 1);
         // ---- arrive (every storing wave drained, then one lane). The builtin tells the waitcnt pass that nothing is
         // pending past this point (the operand loads of the last gather included); the asm keeps the wait where it is
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
@@ -685,15 +652,18 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
             }
                 };
         // the first chunk is peeled and sized to the half's trajectories (idle slots still cost their loads' issue)
-        const int nh = h < TB ? (TB - h + R - 1) / R : 0;  // trajectories of this half
+        // half hg's trajectories are b = hg, hg + R, ...; at R = 2 odd workgroups swap the halves so that half 0 (whose
+        // loads the CU serves first) gathers the trajectories whose outputs this workgroup writes (b = g mod G)
+        const int hg = R == 2 ? (h ^ (g & 1)) : h;
+        const int nh = hg < TB ? (TB - hg + R - 1) / R : 0;  // trajectories of this half
         int fc = 0;
         if constexpr (L::GCH >= 4) {
-            if (nh >= 4) { chunk(MsIC<4>{}, MsIC<1>{}, h); fc = 4; }
+            if (nh >= 4) { chunk(MsIC<4>{}, MsIC<1>{}, hg); fc = 4; }
         }
-        if (fc == 0 && nh >= 2 && L::GCH >= 2) { chunk(MsIC<(L::GCH >= 2 ? 2 : 1)>{}, MsIC<1>{}, h); fc = L::GCH >= 2 ? 2 : 1; }
-        if (fc == 0 && nh >= 1) { chunk(MsIC<1>{}, MsIC<1>{}, h); fc = 1; }
+        if (fc == 0 && nh >= 2 && L::GCH >= 2) { chunk(MsIC<(L::GCH >= 2 ? 2 : 1)>{}, MsIC<1>{}, hg); fc = L::GCH >= 2 ? 2 : 1; }
+        if (fc == 0 && nh >= 1) { chunk(MsIC<1>{}, MsIC<1>{}, hg); fc = 1; }
         if (fc == 0) issue_ops();
-        for (int b0 = h + R * fc; b0 < TB; b0 += R * L::GCH) chunk(MsIC<L::GCH>{}, MsIC<0>{}, b0);
+        for (int b0 = hg + R * fc; b0 < TB; b0 += R * L::GCH) chunk(MsIC<L::GCH>{}, MsIC<0>{}, b0);
         stamp(n, 7);
         wstamp(n, 24);
         __syncthreads();  // r_b from every half before PT(m)
