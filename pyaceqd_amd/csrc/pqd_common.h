@@ -171,6 +171,7 @@ struct MsplitParams {
     int TB, n_groups;        // trajectories per group, groups
     int xcd;                 // > 0: XCD-grouped grid with this many groups per XCD slot; 0: plain grid
     int l2keep;              // 1: payload stores keep their L2 lines (XCD-grouped grid only; placement checked in-kernel)
+    int ptm;                 // 1: PT contraction on the matrix cores (3M, 4 trajectories per row block), 0: FP64 VALU
 };
 
 // ---- free propagators through the pulse windows: M(h), F(n) = M(2n) M(2n-1) and W(n) = ovec . M(2n-1) of system sys

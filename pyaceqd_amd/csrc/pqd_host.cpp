@@ -915,9 +915,9 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
                 total += tr->out_end[t] + 1;
             }
             for (int y = 0; y < n_sys; ++y) shared -= amax[y];
-            // (measured, profiles/r06/: 32 trajectories TB = 1 33 ms vs 124 ms batched; 256 trajectories TB = 8 114 vs
-            // 124 ms; past TB = 8 the per-step gather of TB states per workgroup is not measured to win)
-            const bool want = mode == 2 || (TB <= 8 && 4 * shared <= total);
+            // (measured, profiles/r06/mfma/c4ntraj.log, µs per grid step vs the batched kernel: 32 trajectories TB = 1
+            // 2.9 vs 13.5; 256 TB = 8 6.5 vs 11.8; 384 TB = 12 9.1 vs 11.5; 512 TB = 16 10.9 vs 11.2, about even)
+            const bool want = mode == 2 || (TB <= 12 && 4 * shared <= total);
             // a group's composite MTO steps are held in LDS (pt_msplit.hip s_cev): at most msplit_cev_max() per group
             int max_cev = 0;
             for (int k0 = 0; k0 < tr->n_traj; k0 += TB) {
@@ -1198,8 +1198,12 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
         HIPCHK(P->err.alloc(4));
         // L2-kept exchange lines on the XCD-grouped grid (PQD_MS_L2=0: sc1 stores, as on the plain grid)
         const int l2keep = ms_xcd > 0 && [] { const char* f = getenv("PQD_MS_L2"); return f ? atoi(f) != 0 : true; }();
+        // PT contraction on the matrix cores from 3 trajectories per group (a row block of 4 rows per MFMA; below
+        // that the VALU path's per-trajectory work is smaller); PQD_MS_PTM=0/1 forces the VALU / matrix-core path
+        int ptm = ms_TB >= 3 && P->CHI <= 64;
+        if (const char* f = getenv("PQD_MS_PTM")) ptm = atoi(f) != 0;
         P->mq = MsplitParams{P->ms_gtraj.p, P->ms_gend.p, P->cev_start.p, P->cev.p, P->Fev.p, P->Wev.p,
-                             ms_TB, ms_groups, ms_xcd, l2keep};
+                             ms_TB, ms_groups, ms_xcd, l2keep, ptm};
     }
     HIPCHK(hipStreamSynchronize(s));
     *out = guard.release();

@@ -140,8 +140,9 @@ struct MsLayout {
     static constexpr int TMINE = (TBMAX + G - 1) / G;  // trajectories whose outputs one workgroup writes
     static constexpr int FPT = (R * TBMAX * N2 + NT - 1) / NT;      // F-row entries per thread
     static constexpr int WPT = (TMINE * OMAX * N2 + NT - 1) / NT;   // output-row entries per thread
-    static constexpr int PRO = 0;                        // r_b rows [R][TBMAX][CHI]
-    static constexpr int FRO = PRO + R * TBMAX * CHI;    // F_b(n + 1) rows of the workgroup [R][TBMAX][N2]
+    static constexpr int PRS = CHI + 4;                  // r_b row stride: the MFMA PT's A reads (rows b, k-steps) in distinct banks
+    static constexpr int PRO = 0;                        // r_b rows [R][TBMAX][PRS]
+    static constexpr int FRO = PRO + R * TBMAX * PRS;    // F_b(n + 1) rows of the workgroup [R][TBMAX][N2]
     static constexpr int WLO = FRO + R * TBMAX * N2;     // output rows [TMINE][OMAX][N2]
     static constexpr int CLO = WLO + TMINE * OMAX * N2;  // closure vector of the outputs the gather writes [CHI]
     static constexpr int OPO = CLO + CHI;                // output columns (W row x state, times the closure) [TMINE][OMAX][CHI]
@@ -234,16 +235,20 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
         xtag = xid << 28;
     }
 
-    // thread roles in its half: PT (kq, j): slice rows kq KPER + jj of column j, kq = the lane's 16-lane row, j = 16
-    // (wave in the half) + lane % 16; the gather's roles are set in the step loop
+    // thread roles in its half: PT column j = 16 (wave in the half) + lane % 16 and the lane's 16-lane row kq. The
+    // VALU PT (q.ptm = 0) holds slice rows kq KPER + jj of column j; the matrix-core PT (q.ptm = 1) holds rows
+    // 4 jj + kq, the B operand of v_mfma_f64_4x4x4_4b at k-step jj (lane 16 k + 4 blk + x: B[blk][k][x] = S[4 jj + k]
+    // [16 w + 4 blk + x]). The gather's roles are set in the step loop
     const int kq = (ht & 63) >> 4, j = 16 * (ht >> 6) + (ht & 15);
     const int grow = live ? p.gmap[alpha] : 0;
+    const bool ptm = CHI <= 64 && q.ptm != 0;  // (chi = 128: the VALU path only; its slice row alone is 128 VGPRs)
     double2 sreg[KPER];
     auto fetch_slice = [&](int si) {
         if (!live) return;
         const double2* __restrict__ S = p.Q + ((size_t)si * p.D + grow) * CHI * CHI;
 #pragma unroll
-        for (int jj = 0; jj < KPER; ++jj) sreg[jj] = ms_gld(S + (size_t)(kq * KPER + jj) * CHI + j);
+        for (int jj = 0; jj < KPER; ++jj)
+            sreg[jj] = ms_gld(S + (size_t)(ptm ? 4 * jj + kq : kq * KPER + jj) * CHI + j);
     };
     // the schedule, 64 entries per VGPR (lane i holds sched[64 c + i]) one chunk ahead, picked with v_readlane
     auto sched_chunk = [&](int ch) {
@@ -268,7 +273,7 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
             (ci >= 0 ? q.Fev + (size_t)ci * m2 : fw_M(p, sy, fw_win(p, sy), 0, m2)) + (size_t)a * N2;
         double2 acc = c_zero();
         for (int be = 0; be < N2; ++be) c_fma(acc, ms_gld(Fr + be), ms_gld(p.rho0 + be));
-        smem[L::PRO + (r * TBM + b) * CHI + k] = c_mul(acc, ms_gld(p.bond0 + k));
+        smem[L::PRO + (r * TBM + b) * L::PRS + k] = c_mul(acc, ms_gld(p.bond0 + k));
     }
     for (int e = tid; e < TB * n_out; e += NT) {
         const int b = e / n_out, k = e - b * n_out;
@@ -451,7 +456,42 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
         // row value kq KPER + 16 c + i (one ds_read_b128 per wave and 64 values), the products take it by DPP
         // row_newbcast, two permlane swaps add the k-groups, and row 0 stores the 16 columns — no LDS partials and no
         // barrier between the PT and the publish. The row values of PF trajectories are read at once
-        if (live) {
+        if (live && ptm) {
+            // on the matrix cores, three real products per complex product (3M: P1 = Xr Sr, P2 = Xi Si, P3 = (Xr + Xi)
+            // (Sr + Si); y = (P1 - P2, P3 - P1 - P2)), two row blocks of 4 trajectories per pass: lane 16 k + 4 blk + x
+            // reads A = X[4 rb + x][4 jj + k] (rows PRS apart: distinct banks) and ends up holding y[4 rb + k][j]. Rows
+            // of slots past TB or inactive are contracted too (each output row depends on its own input row only) and
+            // not stored
+            const int x = lane & 3;
+            const double2* __restrict__ xr = smem + L::PRO + h * TBM * L::PRS + kq;
+            for (int rb0 = 0; rb0 < TB; rb0 += 8) {
+                double p1[2] = {0.0, 0.0}, p2[2] = {0.0, 0.0}, p3[2] = {0.0, 0.0};
+                const bool two = rb0 + 4 < TB;
+#pragma unroll
+                for (int jj = 0; jj < KPER; ++jj) {
+                    const double qs = sreg[jj].x + sreg[jj].y;
+                    const double2 a0 = xr[(rb0 + x) * L::PRS + 4 * jj];
+                    p1[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(a0.x, sreg[jj].x, p1[0], 0, 0, 0);
+                    p2[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(a0.y, sreg[jj].y, p2[0], 0, 0, 0);
+                    p3[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(a0.x + a0.y, qs, p3[0], 0, 0, 0);
+                    if (two) {
+                        const double2 a1 = xr[(rb0 + 4 + x) * L::PRS + 4 * jj];
+                        p1[1] = __builtin_amdgcn_mfma_f64_4x4x4f64(a1.x, sreg[jj].x, p1[1], 0, 0, 0);
+                        p2[1] = __builtin_amdgcn_mfma_f64_4x4x4f64(a1.y, sreg[jj].y, p2[1], 0, 0, 0);
+                        p3[1] = __builtin_amdgcn_mfma_f64_4x4x4f64(a1.x + a1.y, qs, p3[1], 0, 0, 0);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int b = rb0 + 4 * u + kq;
+                    if (b < TB && ((act >> b) & 1)) {
+                        double2* dst = Xg + ((size_t)b * 2 + (n & 1)) * E + (size_t)alpha * CHI + j;
+                        const double2 y = make_double2(p1[u] - p2[u], p3[u] - p1[u] - p2[u]);
+                        if (q.l2keep) ms_st_keep(dst, y); else ms_st_sc1(dst, y);
+                    }
+                }
+            }
+        } else if (live) {
             constexpr int PF = CHI <= 32 ? 8 : (CHI <= 64 ? 4 : 1);
             for (int b0 = 0; b0 < TB; b0 += PF) {
                 double2 pv[PF][L::PVR];
@@ -460,7 +500,7 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
 #pragma unroll
                     for (int c = 0; c < L::PVR; ++c) {
                         const int jv = 16 * c + (lane & 15), bu = b0 + u < TBM ? b0 + u : TBM - 1;
-                        pv[u][c] = smem[L::PRO + (h * TBM + bu) * CHI + kq * KPER + (jv < KPER ? jv : KPER - 1)];
+                        pv[u][c] = smem[L::PRO + (h * TBM + bu) * L::PRS + kq * KPER + (jv < KPER ? jv : KPER - 1)];
                     }
 #pragma unroll
                 for (int u = 0; u < PF; ++u) {
@@ -627,7 +667,7 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
                         for (int i = 0; i < EPT; ++i)
                             if (rg + RG * i < N2) c_fma(part, fv[i], xv[i]);
                         part = ms_rg_sum<KPER>(part);
-                        if (rg == 0) smem[L::PRO + (r * TBM + b) * CHI + kcol] = part;
+                        if (rg == 0) smem[L::PRO + (r * TBM + b) * L::PRS + kcol] = part;
                     }
                 }
                 if ((own >> b) & 1) {

@@ -214,3 +214,26 @@ def test_msplit_spread_group_reruns_with_sc1_stores(monkeypatch):
     plan.execute()  # stays on sc1 stores: no further fallback
     cmp_lists(plan.download(), got, 1e-15)
     assert plan.info()[2] == 1
+
+
+@pytest.mark.parametrize("N,chi", [(3, 32), (4, 64), (5, 32), (6, 64)])
+@pytest.mark.parametrize("ptm", ["0", "1"])
+@pytest.mark.parametrize("tb", ["1", "5", "8"])
+def test_msplit_pt_on_valu_and_matrix_cores(monkeypatch, N, chi, ptm, tb):
+    """the PT contraction on the FP64 VALU (DPP row broadcast) and on the matrix cores (3M 4x4x4_4b row blocks,
+    PQD_MS_PTM), with partial row blocks (TB = 1, 5) and inactive slots, vs the oracle"""
+    monkeypatch.setenv("PQD_MSPLIT", "2")
+    monkeypatch.setenv("PQD_MS_PTM", ptm)
+    monkeypatch.setenv("PQD_MS_TB", tb)
+    systems = [H.random_system(N, n_steps=36, seed=90 + k)[0] for k in range(2)]
+    grid = Grid(0.0, 0.1, 36)
+    tr = mixed_trajectories(grid.n_steps, N, 19, seed=N + 7 * chi)
+    tr.system = np.array([k % 2 for k in range(19)])
+    pt = ptmod.random_pt(N, chi, D=min(N * N, 9), n_slices=8, seed=chi + 3 * N, eps=0.15)
+    ops = [H.ketbra(N, 0, 0), H.ketbra(N, 1, 0), np.eye(N)]
+    rho0 = H.random_rho(N)
+    plan = engine.Plan(systems, grid, rho0, ops, tr, pt=pt)
+    plan.execute()
+    got = plan.download()
+    assert plan.info()[0] == MSPLIT and plan.info()[2] == 0
+    cmp_lists(got, oracle.propagate(systems, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
