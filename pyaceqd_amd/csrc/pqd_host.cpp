@@ -915,9 +915,9 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
                 total += tr->out_end[t] + 1;
             }
             for (int y = 0; y < n_sys; ++y) shared -= amax[y];
-            // (measured, profiles/r06/mfma/c4ntraj.log, µs per grid step vs the batched kernel: 32 trajectories TB = 1
-            // 2.9 vs 13.5; 256 TB = 8 6.5 vs 11.8; 384 TB = 12 9.1 vs 11.5; 512 TB = 16 10.9 vs 11.2, about even)
-            const bool want = mode == 2 || (TB <= 12 && 4 * shared <= total);
+            // (measured, profiles/r06/bfly/c4ntraj.log, µs per grid step vs the batched kernel: 32 trajectories TB = 1
+            // 2.8 vs 13.5; 256 TB = 8 6.0 vs 11.8; 384 TB = 12 8.3 vs 11.5; 512 TB = 16 9.8 vs 11.1)
+            const bool want = mode == 2 || (TB <= 16 && 4 * shared <= total);
             // a group's composite MTO steps are held in LDS (pt_msplit.hip s_cev): at most msplit_cev_max() per group
             int max_cev = 0;
             for (int k0 = 0; k0 < tr->n_traj; k0 += TB) {

@@ -102,6 +102,23 @@ __device__ __forceinline__ double2 ms_rg_sum(double2 v) {
     }
 }
 
+// two sums over the 4 row groups of a gather column at KPER >= 16 (row groups = 16-lane rows): the lanes of the even
+// row groups get a's sum, those of the odd ones b's. v_permlane16_swap exchanges the odd 16-lane rows of its first
+// operand with the even rows of its second, so after swapping (a, b) an even row holds a and its odd neighbour's a,
+// an odd row b and its even neighbour's b; one permlane32 sum then adds the other pair (the same grouping, and bits,
+// as two ms_rg_sum calls, at half their instructions)
+__device__ __forceinline__ double ms_pair16(double u, double v) {
+    const long long U = __double_as_longlong(u), V = __double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)U, (unsigned)V, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(U >> 32), (unsigned)(V >> 32), false, false);
+    return __longlong_as_double(((long long)hi[0] << 32) | (unsigned)lo[0]) +
+           __longlong_as_double(((long long)hi[1] << 32) | (unsigned)lo[1]);
+}
+__device__ __forceinline__ double2 ms_rg_sum2(double2 a, double2 b) {
+    const double2 h = make_double2(ms_pair16(a.x, b.x), ms_pair16(a.y, b.y));
+    return make_double2(xor_add<32>(h.x), xor_add<32>(h.y));
+}
+
 // plain 16-B global store: the line stays in the XCD's L2 (an sc1 store drops it, and the same-XCD readers then fetch
 // it at the cross-XCD rate, MI355X_MICROARCH.md § visibility, store flavours). Used only where every workgroup of the
 // group runs on one XCD (checked at the first poll: see l2keep)
@@ -653,40 +670,82 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
                 // the operand entries of a row are read from LDS together and then used (read one by one next to
                 // their products, each read's latency was exposed: ≈9,300 cycles for 8 trajectories' rows)
                 if ((nxt >> b) & 1) {
+                    if constexpr (R == 2 && KPER >= 16 && EPT <= 4) {
+                        // both rows at once: one butterfly sums row 0 into the even row groups and row 1 into the odd
+                        // ones (ms_rg_sum2), and one store writes both
+                        double2 part[2] = {c_zero(), c_zero()};
 #pragma unroll
-                    for (int r = 0; r < R; ++r) {
-                        if (R * g + r >= N2) continue;
-                        double2 fv[EPT];
+                        for (int r = 0; r < 2; ++r) {
+                            double2 fv[EPT];
 #pragma unroll
-                        for (int i = 0; i < EPT; ++i) {
-                            const int be = rg + RG * i;
-                            fv[i] = smem[L::FRO + (r * TBM + b) * N2 + (be < N2 ? be : 0)];
+                            for (int i = 0; i < EPT; ++i) {
+                                const int be = rg + RG * i;
+                                fv[i] = smem[L::FRO + (r * TBM + b) * N2 + (be < N2 ? be : 0)];
+                            }
+#pragma unroll
+                            for (int i = 0; i < EPT; ++i)
+                                if (rg + RG * i < N2) c_fma(part[r], fv[i], xv[i]);
                         }
-                        double2 part = c_zero();
+                        const double2 sum = ms_rg_sum2(part[0], part[1]);
+                        if (rg < 2 && 2 * g + rg < N2) smem[L::PRO + (rg * TBM + b) * L::PRS + kcol] = sum;
+                    } else {
 #pragma unroll
-                        for (int i = 0; i < EPT; ++i)
-                            if (rg + RG * i < N2) c_fma(part, fv[i], xv[i]);
-                        part = ms_rg_sum<KPER>(part);
-                        if (rg == 0) smem[L::PRO + (r * TBM + b) * L::PRS + kcol] = part;
+                        for (int r = 0; r < R; ++r) {
+                            if (R * g + r >= N2) continue;
+                            double2 fv[EPT];
+#pragma unroll
+                            for (int i = 0; i < EPT; ++i) {
+                                const int be = rg + RG * i;
+                                fv[i] = smem[L::FRO + (r * TBM + b) * N2 + (be < N2 ? be : 0)];
+                            }
+                            double2 part = c_zero();
+#pragma unroll
+                            for (int i = 0; i < EPT; ++i)
+                                if (rg + RG * i < N2) c_fma(part, fv[i], xv[i]);
+                            part = ms_rg_sum<KPER>(part);
+                            if (rg == 0) smem[L::PRO + (r * TBM + b) * L::PRS + kcol] = part;
+                        }
                     }
                 }
                 if ((own >> b) & 1) {
                     // output column kcol of W(m)[k] . Q times the closure: like a row of r_b, the sum over columns
                     // is left to flush (next step, while wave 0 polls)
                     const int mb = b / G;
-                    for (int k = 0; k < n_out; ++k) {
-                        double2 wv[EPT];
+                    if constexpr (KPER >= 16 && EPT <= 4) {
+                        // two outputs per butterfly (k0 in the even row groups, k0 + 1 in the odd ones)
+                        for (int k0 = 0; k0 < n_out; k0 += 2) {
+                            double2 o[2] = {c_zero(), c_zero()};
 #pragma unroll
-                        for (int i = 0; i < EPT; ++i) {
-                            const int be = rg + RG * i;
-                            wv[i] = smem[L::WLO + (mb * L::OMAX + k) * N2 + (be < N2 ? be : 0)];
+                            for (int u = 0; u < 2; ++u) {
+                                double2 wv[EPT];
+#pragma unroll
+                                for (int i = 0; i < EPT; ++i) {
+                                    const int be = rg + RG * i;
+                                    wv[i] = smem[L::WLO + (mb * L::OMAX + k0 + u) * N2 + (be < N2 ? be : 0)];
+                                }
+#pragma unroll
+                                for (int i = 0; i < EPT; ++i)
+                                    if (rg + RG * i < N2) c_fma(o[u], wv[i], xv[i]);
+                            }
+                            const double2 sum = ms_rg_sum2(o[0], o[1]);
+                            if (rg < 2 && k0 + rg < n_out)
+                                smem[L::OPO + (mb * L::OMAX + k0 + rg) * CHI + kcol] = c_mul(sum, cv);
                         }
-                        double2 o = c_zero();
+                    } else {
+                        for (int k = 0; k < n_out; ++k) {
+                            double2 wv[EPT];
 #pragma unroll
-                        for (int i = 0; i < EPT; ++i)
-                            if (rg + RG * i < N2) c_fma(o, wv[i], xv[i]);
-                        o = ms_rg_sum<KPER>(o);
-                        if (rg == 0) smem[L::OPO + (mb * L::OMAX + k) * CHI + kcol] = c_mul(o, cv);
+                            for (int i = 0; i < EPT; ++i) {
+                                const int be = rg + RG * i;
+                                wv[i] = smem[L::WLO + (mb * L::OMAX + k) * N2 + (be < N2 ? be : 0)];
+                            }
+                            double2 o = c_zero();
+#pragma unroll
+                            for (int i = 0; i < EPT; ++i)
+                                if (rg + RG * i < N2) c_fma(o, wv[i], xv[i]);
+                            o = ms_rg_sum<KPER>(o);
+                            if (rg == 0) smem[L::OPO + (mb * L::OMAX + k) * CHI + kcol] = c_mul(o, cv);
+                        }
                     }
                 }
             }
