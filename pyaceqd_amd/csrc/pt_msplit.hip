@@ -653,13 +653,15 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
                 __builtin_amdgcn_sched_barrier(0);
                 stamp(n, 5);
             }
+            // each trajectory's loads are waited for right before its arithmetic (in issue order: the counted
+            // vmcnt leaves the later trajectories' loads in flight) and on every path, used or not
 #pragma unroll
-            for (int bb = 0; bb < GC; ++bb)
-#pragma unroll
-                for (int i = 0; i < EPT; ++i) asm volatile("" ::"v"(xr[bb][i]));
+            for (int i = 0; i < EPT; ++i) asm volatile("" ::"v"(xr[0][i]));
             if constexpr (FIRST) { stamp(n, 6); wstamp(n, 16); }
 #pragma unroll
             for (int bb = 0; bb < GC; ++bb) {
+#pragma unroll
+                for (int i = 0; i < EPT; ++i) asm volatile("" ::"v"(xr[bb][i]));
                 const int b = slot_b(bb);
                 if (b >= TB || !((act >> b) & 1)) continue;
                 double2 xv[EPT];
