@@ -759,7 +759,9 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
         const int nh = hg < TB ? (TB - hg + R - 1) / R : 0;  // trajectories of this half
         int fc = 0;
         if constexpr (L::GCH >= 4) {
-            if (nh >= 4) { chunk(MsIC<4>{}, MsIC<1>{}, hg); fc = 4; }
+            // (three trajectories too: one idle slot, one round trip; a chunk of 2 and one of 4 with 3 idle slots
+            // took two, and a third chunk size made the compiler spill ≈1,000 VGPRs)
+            if (nh >= 3) { chunk(MsIC<4>{}, MsIC<1>{}, hg); fc = 4; }
         }
         if (fc == 0 && nh >= 2 && L::GCH >= 2) { chunk(MsIC<(L::GCH >= 2 ? 2 : 1)>{}, MsIC<1>{}, hg); fc = L::GCH >= 2 ? 2 : 1; }
         if (fc == 0 && nh >= 1) { chunk(MsIC<1>{}, MsIC<1>{}, hg); fc = 1; }
