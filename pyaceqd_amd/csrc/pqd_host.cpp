@@ -77,6 +77,7 @@ int pad_chi(int chi) {
     if (chi <= 32) return 32;
     if (chi <= 64) return 64;
     if (chi <= 128) return 128;
+    if (chi <= 256) return 256;  // multi-trajectory split groups only (pt_msplit.hip, slice rows streamed)
     return -1;
 }
 
@@ -394,7 +395,7 @@ int pqd_pt_create(pqd_ctx* ctx, int32_t dim, const pqd_pt_desc* d, pqd_pt** out)
     if (dim < 2 || dim > 6) return fail(PQD_ERR_UNSUPPORTED, "dim %d", dim);
     const int N2 = dim * dim;
     const int CHI = pad_chi(d->chi);
-    if (d->chi < 1 || CHI < 0) return fail(PQD_ERR_UNSUPPORTED, "chi %d not in [1, 128]", d->chi);
+    if (d->chi < 1 || CHI < 0) return fail(PQD_ERR_UNSUPPORTED, "chi %d not in [1, 256]", d->chi);
     if (d->D < 1 || d->n_slices < 1) return fail(PQD_ERR_ARG, "D and n_slices must be >= 1");
     if (!d->Q || !d->closure || !d->closure0 || !d->bond0 || !d->gmap) return fail(PQD_ERR_ARG, "NULL PT array");
     for (int a = 0; a < N2; ++a)
@@ -689,7 +690,8 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     if (pt) {
         if (pt->ctx != ctx) return fail(PQD_ERR_ARG, "PT belongs to another context");
         if (pt->dim != N) return fail(PQD_ERR_ARG, "PT dim %d != system dim %d", pt->dim, N);
-        if (!sweep_supported(N2, pt->CHI)) return fail(PQD_ERR_UNSUPPORTED, "N2=%d CHI=%d", N2, pt->CHI);
+        if (!sweep_supported(N2, pt->CHI) && !(pt->CHI == 256 && msplit_supported(N2, pt->CHI, n_out)))
+            return fail(PQD_ERR_UNSUPPORTED, "N2=%d CHI=%d (chi 256: N2 4, 9 or 16 and at most 8 outputs)", N2, pt->CHI);
     }
     for (int t = 0; t < tr->n_traj; ++t) {
         const int b = tr->out_begin[t], e = tr->out_end[t];
@@ -891,6 +893,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
         // PQD_SPLIT=0 (batched kernel only) and a forced trunk pre-pass (PQD_TRUNK=1) keep the batched path
         if (const char* sp0 = getenv("PQD_SPLIT"); sp0 && atoi(sp0) == 0) mode = 0;
         if (const char* tk = getenv("PQD_TRUNK"); tk && atoi(tk) == 1 && mode == 1) mode = 0;
+        if (pt && P->CHI == 256) mode = 2;  // no other path holds chi = 256
         const int bpc = (pt && !P->split && mode != 0 && fuse_on && tr->n_traj >= 1 && msplit_supported(N2, P->CHI, n_out))
                             ? msplit_blocks_per_cu(N2, P->CHI) : 0;
         if (bpc >= 1) {
@@ -938,6 +941,10 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
             }
         }
     }
+    if (pt && P->CHI == 256 && !P->msplit)
+        return fail(PQD_ERR_UNSUPPORTED, "chi 256 runs on multi-trajectory split groups only: %d trajectories at N2=%d do "
+                    "not fit one launch of them (at most 8 per group), or the plan has no fused steps (PQD_FUSE=0)",
+                    tr->n_traj, N2);
     const bool branch_on = P->branch != 0 && pt != nullptr && !P->split && !P->msplit;
     // blocks are filled in this order and may straddle systems (each wave indexes its own system's propagators),
     // so a scan with one trajectory per system still fills every slot of a workgroup
@@ -1284,6 +1291,9 @@ int pqd_plan_synchronize(pqd_plan* P) {
             HIPCHK(hipMemcpyAsync(err, P->err.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
         }
+        if (err[0] && P->msplit && P->CHI > 128)
+            return fail(PQD_ERR_HIP, "multi-trajectory split groups timed out at chi %d (no batched fallback holds that "
+                        "bond); the device is shared or the groups could not all be resident", P->CHI);
         if (err[0]) {
             P->split = false;
             P->msplit = false;

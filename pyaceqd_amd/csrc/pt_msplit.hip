@@ -258,9 +258,13 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
     // [16 w + 4 blk + x]). The gather's roles are set in the step loop
     const int kq = (ht & 63) >> 4, j = 16 * (ht >> 6) + (ht & 15);
     const int grow = live ? p.gmap[alpha] : 0;
-    const bool ptm = CHI <= 64 && q.ptm != 0;  // (chi = 128: the VALU path only; its slice row alone is 128 VGPRs)
-    double2 sreg[KPER];
+    // chi = 128: the VALU path only (its slice row alone is 128 VGPRs); chi = 256 (STREAM): the slice row (1 MiB) is
+    // streamed from L2 through the matrix-core PT every step, 4 k-steps at a time, and sreg is unused
+    constexpr bool STREAM = CHI > 128;
+    const bool ptm = STREAM || (CHI <= 64 && q.ptm != 0);
+    double2 sreg[STREAM ? 1 : KPER];
     auto fetch_slice = [&](int si) {
+        if constexpr (STREAM) return;
         if (!live) return;
         const double2* __restrict__ S = p.Q + ((size_t)si * p.D + grow) * CHI * CHI;
 #pragma unroll
@@ -484,19 +488,35 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
             for (int rb0 = 0; rb0 < TB; rb0 += 8) {
                 double p1[2] = {0.0, 0.0}, p2[2] = {0.0, 0.0}, p3[2] = {0.0, 0.0};
                 const bool two = rb0 + 4 < TB;
-#pragma unroll
-                for (int jj = 0; jj < KPER; ++jj) {
-                    const double qs = sreg[jj].x + sreg[jj].y;
+                auto kstep = [&](int jj, double2 bv) {
+                    const double qs = bv.x + bv.y;
                     const double2 a0 = xr[(rb0 + x) * L::PRS + 4 * jj];
-                    p1[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(a0.x, sreg[jj].x, p1[0], 0, 0, 0);
-                    p2[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(a0.y, sreg[jj].y, p2[0], 0, 0, 0);
+                    p1[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(a0.x, bv.x, p1[0], 0, 0, 0);
+                    p2[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(a0.y, bv.y, p2[0], 0, 0, 0);
                     p3[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(a0.x + a0.y, qs, p3[0], 0, 0, 0);
                     if (two) {
                         const double2 a1 = xr[(rb0 + 4 + x) * L::PRS + 4 * jj];
-                        p1[1] = __builtin_amdgcn_mfma_f64_4x4x4f64(a1.x, sreg[jj].x, p1[1], 0, 0, 0);
-                        p2[1] = __builtin_amdgcn_mfma_f64_4x4x4f64(a1.y, sreg[jj].y, p2[1], 0, 0, 0);
+                        p1[1] = __builtin_amdgcn_mfma_f64_4x4x4f64(a1.x, bv.x, p1[1], 0, 0, 0);
+                        p2[1] = __builtin_amdgcn_mfma_f64_4x4x4f64(a1.y, bv.y, p2[1], 0, 0, 0);
                         p3[1] = __builtin_amdgcn_mfma_f64_4x4x4f64(a1.x + a1.y, qs, p3[1], 0, 0, 0);
                     }
+                };
+                if constexpr (STREAM) {
+                    // B = S[4 jj + kq][j] of this row's slice, 4 k-steps of loads at a time (L2-resident: every
+                    // workgroup of the step reads the same slices)
+                    const double2* __restrict__ Sg =
+                        p.Q + ((size_t)cur_slice * p.D + grow) * CHI * CHI + (size_t)kq * CHI + j;
+                    constexpr int PFS = 4;
+                    for (int j0 = 0; j0 < KPER; j0 += PFS) {
+                        double2 bq[PFS];
+#pragma unroll
+                        for (int u = 0; u < PFS; ++u) bq[u] = ms_gld(Sg + (size_t)4 * (j0 + u) * CHI);
+#pragma unroll
+                        for (int u = 0; u < PFS; ++u) kstep(j0 + u, bq[u]);
+                    }
+                } else {
+#pragma unroll
+                    for (int jj = 0; jj < KPER; ++jj) kstep(jj, sreg[jj]);
                 }
 #pragma unroll
                 for (int u = 0; u < 2; ++u) {
@@ -508,29 +528,32 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
                     }
                 }
             }
-        } else if (live) {
-            constexpr int PF = CHI <= 32 ? 8 : (CHI <= 64 ? 4 : 1);
-            for (int b0 = 0; b0 < TB; b0 += PF) {
-                double2 pv[PF][L::PVR];
+        }
+        if constexpr (!STREAM) {
+            if (live && !ptm) {
+                constexpr int PF = CHI <= 32 ? 8 : (CHI <= 64 ? 4 : 1);
+                for (int b0 = 0; b0 < TB; b0 += PF) {
+                    double2 pv[PF][L::PVR];
 #pragma unroll
-                for (int u = 0; u < PF; ++u)
+                    for (int u = 0; u < PF; ++u)
 #pragma unroll
-                    for (int c = 0; c < L::PVR; ++c) {
-                        const int jv = 16 * c + (lane & 15), bu = b0 + u < TBM ? b0 + u : TBM - 1;
-                        pv[u][c] = smem[L::PRO + (h * TBM + bu) * L::PRS + kq * KPER + (jv < KPER ? jv : KPER - 1)];
-                    }
+                        for (int c = 0; c < L::PVR; ++c) {
+                            const int jv = 16 * c + (lane & 15), bu = b0 + u < TBM ? b0 + u : TBM - 1;
+                            pv[u][c] = smem[L::PRO + (h * TBM + bu) * L::PRS + kq * KPER + (jv < KPER ? jv : KPER - 1)];
+                        }
 #pragma unroll
-                for (int u = 0; u < PF; ++u) {
-                    const int b = b0 + u;
-                    if (b >= TB || !((act >> b) & 1)) continue;
-                    double2 acc = c_zero();
-                    ms_nop_for(pv[u]);
-                    ms_pt_bcast<0, KPER>(acc, pv[u], sreg);
-                    acc = make_double2(xor_add<16>(acc.x), xor_add<16>(acc.y));
-                    acc = make_double2(xor_add<32>(acc.x), xor_add<32>(acc.y));
-                    if (lane < 16) {
-                        double2* dst = Xg + ((size_t)b * 2 + (n & 1)) * E + (size_t)alpha * CHI + j;
-                        if (q.l2keep) ms_st_keep(dst, acc); else ms_st_sc1(dst, acc);
+                    for (int u = 0; u < PF; ++u) {
+                        const int b = b0 + u;
+                        if (b >= TB || !((act >> b) & 1)) continue;
+                        double2 acc = c_zero();
+                        ms_nop_for(pv[u]);
+                        ms_pt_bcast<0, KPER>(acc, pv[u], sreg);
+                        acc = make_double2(xor_add<16>(acc.x), xor_add<16>(acc.y));
+                        acc = make_double2(xor_add<32>(acc.x), xor_add<32>(acc.y));
+                        if (lane < 16) {
+                            double2* dst = Xg + ((size_t)b * 2 + (n & 1)) * E + (size_t)alpha * CHI + j;
+                            if (q.l2keep) ms_st_keep(dst, acc); else ms_st_sc1(dst, acc);
+                        }
                     }
                 }
             }
@@ -617,9 +640,9 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
         } else if constexpr (KPER == 16) {
             rg = gl >> 4;
             kcol = gw * KPER + (gl & 15);
-        } else {
+        } else {  // KPER = 32 / 64: a k-group spans KPER / 16 waves
             rg = gl >> 4;
-            kcol = (gw >> 1) * KPER + 16 * (gw & 1) + (gl & 15);
+            kcol = (gw / (KPER / 16)) * KPER + 16 * (gw % (KPER / 16)) + (gl & 15);
         }
         const double2 cv = smem[L::CLO + kcol];
         auto chunk = [&](auto gct, auto firstt, int b0) {
@@ -868,6 +891,9 @@ constexpr int ms_rows(int N2) { return N2 == 9 ? 1 : 2; }
 template <int N2>
 hipError_t launch_ms_n(int CHI, const SweepParams& p, const MsplitParams& q, double2* X, unsigned* cnt,
                        unsigned* err, hipStream_t s) {
+    if constexpr (N2 == 4) {  // chi = 256 only
+        return CHI == 256 ? launch_ms_t<4, 256, 1>(p, q, X, cnt, err, s) : hipErrorInvalidValue;
+    } else {
     switch (CHI) {
         case 32: return launch_ms_t<N2, 32, ms_rows(N2)>(p, q, X, cnt, err, s);
         case 64:
@@ -876,12 +902,19 @@ hipError_t launch_ms_n(int CHI, const SweepParams& p, const MsplitParams& q, dou
         case 128:
             if constexpr (N2 <= 16) return launch_ms_t<N2, 128, 1>(p, q, X, cnt, err, s);
             return hipErrorInvalidValue;
+        case 256:
+            if constexpr (N2 <= 16) return launch_ms_t<N2, 256, 1>(p, q, X, cnt, err, s);
+            return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
+    }
     }
 }
 
 template <int N2>
 int ms_occ_n(int CHI) {
+    if constexpr (N2 == 4) {
+        return CHI == 256 ? ms_occ_t<4, 256, 1>() : 0;
+    } else {
     switch (CHI) {
         case 32: return ms_occ_t<N2, 32, ms_rows(N2)>();
         case 64:
@@ -890,13 +923,18 @@ int ms_occ_n(int CHI) {
         case 128:
             if constexpr (N2 <= 16) return ms_occ_t<N2, 128, 1>();
             return 0;
+        case 256:
+            if constexpr (N2 <= 16) return ms_occ_t<N2, 256, 1>();
+            return 0;
         default: return 0;
+    }
     }
 }
 
 }  // namespace
 
 int msplit_rows(int N2, int CHI) { return CHI > 64 ? 1 : ms_rows(N2); }
+// (N2 = 4 only at chi = 256: the two-level system's other bonds run on the quad and batched kernels)
 int msplit_tbmax(int N2, int CHI) { return CHI > 64 ? 8 : (ms_rows(N2) == 1 ? 32 : 16); }
 int msplit_cev_max() { return MS_CEV_MAX; }
 int msplit_group_size(int N2, int CHI) { return (N2 + msplit_rows(N2, CHI) - 1) / msplit_rows(N2, CHI); }
@@ -905,12 +943,16 @@ bool msplit_supported(int N2, int CHI, int n_out) {
     // N2 = 25 at chi = 64 spills (7 gathered rows per thread for two PT rows): the single split or batched kernels
     // chi = 128 (the bond cap of generated N <= 4 PTs, which the single-trajectory split kernel does not take): one PT
     // row per workgroup of 512 threads, the 256 KiB slice row in their registers
+    // chi = 256 (a bond past the batched kernel's LDS: generated PTs whose threshold asks for more than 128, VERDICT r5
+    // item 2b): one PT row per workgroup of 1,024 threads, the slice row streamed from L2 each step
+    if (CHI == 256) return (N2 == 4 || N2 == 9 || N2 == 16) && n_out >= 1 && n_out <= 8;
     return (N2 == 9 || N2 == 16 || N2 == 25 || N2 == 36) &&
            (CHI == 32 || (CHI == 64 && N2 != 25) || (CHI == 128 && N2 <= 16)) && n_out >= 1 && n_out <= 8;
 }
 
 int msplit_blocks_per_cu(int N2, int CHI) {
     switch (N2) {
+        case 4: return ms_occ_n<4>(CHI);
         case 9: return ms_occ_n<9>(CHI);
         case 16: return ms_occ_n<16>(CHI);
         case 25: return ms_occ_n<25>(CHI);
@@ -923,6 +965,7 @@ hipError_t launch_evcomp(int N2, const SweepParams& p, const MsplitParams& q, in
     if (n_cev <= 0) return hipSuccess;
     const dim3 grid((unsigned)(n_cev < 4096 ? n_cev : 4096));
     switch (N2) {
+        case 4: hipLaunchKernelGGL((evcomp_kernel<4>), grid, dim3(256), 0, s, p, q, n_cev, n_steps); break;
         case 9: hipLaunchKernelGGL((evcomp_kernel<9>), grid, dim3(256), 0, s, p, q, n_cev, n_steps); break;
         case 16: hipLaunchKernelGGL((evcomp_kernel<16>), grid, dim3(256), 0, s, p, q, n_cev, n_steps); break;
         case 25: hipLaunchKernelGGL((evcomp_kernel<25>), grid, dim3(256), 0, s, p, q, n_cev, n_steps); break;
@@ -940,6 +983,7 @@ hipError_t launch_msplit(int N2, int CHI, const SweepParams& p, const MsplitPara
     e = hipMemsetAsync(err, 0, 4 * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
     switch (N2) {
+        case 4: return launch_ms_n<4>(CHI, p, q, X, cnt, err, s);
         case 9: return launch_ms_n<9>(CHI, p, q, X, cnt, err, s);
         case 16: return launch_ms_n<16>(CHI, p, q, X, cnt, err, s);
         case 25: return launch_ms_n<25>(CHI, p, q, X, cnt, err, s);

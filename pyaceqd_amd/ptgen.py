@@ -465,7 +465,14 @@ def generation_key(boson_op, dt, t_mem, ae, temperature, threshold, factor_ah, b
 
 
 def default_max_bond(boson_op):
-    """the sweep kernel's LDS-resident bond: 128 for N <= 4, 64 above"""
+    """the bond cap of generated PTs: 128 for N <= 4, 64 above — the batched sweep kernel's LDS-resident bond
+    (DESIGN.md §4). PQD_PT_MAX_BOND overrides it (0: no cap): bonds up to 256 at N <= 4 run on multi-trajectory
+    split groups with the slice rows streamed (pt_msplit.hip, at most 8 trajectories per group), so a caller's
+    threshold can decide the cut where the cap would (the cut is recorded in meta['truncation'])"""
+    import os
+    env = os.environ.get("PQD_PT_MAX_BOND")
+    if env is not None and env.strip() != "":
+        return int(env)
     return 128 if np.asarray(boson_op).shape[0] <= 4 else 64
 
 

@@ -237,3 +237,33 @@ def test_msplit_pt_on_valu_and_matrix_cores(monkeypatch, N, chi, ptm, tb):
     got = plan.download()
     assert plan.info()[0] == MSPLIT and plan.info()[2] == 0
     cmp_lists(got, oracle.propagate(systems, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
+
+
+@pytest.mark.parametrize("N,n_traj,chi", [(2, 1, 200), (2, 9, 256), (3, 4, 160), (4, 1, 256), (4, 6, 180)])
+def test_msplit_chi256_vs_oracle(N, n_traj, chi):
+    """bonds past 128 (padded to 256: the slice rows streamed from L2 through the matrix-core PT, one PT row per
+    workgroup of 1,024 threads) for the two-level system (N2 = 4, the only path that holds it), N = 3 and the biexciton,
+    single and several trajectories per group, MTOs, vs the oracle (a path that holds a bond the
+    generator's cap would otherwise cut)"""
+    systems = [H.random_system(N, n_steps=24, seed=70 + k)[0] for k in range(2)]
+    grid = Grid(0.0, 0.1, 24)
+    tr = mixed_trajectories(grid.n_steps, N, n_traj, seed=N + chi)
+    tr.system = np.array([k % 2 for k in range(n_traj)])
+    pt = ptmod.random_pt(N, chi, D=min(N * N, 9), n_slices=5, seed=N + chi, eps=0.15)
+    ops = [H.ketbra(N, 0, 0), H.ketbra(N, 1, 0), np.eye(N)]
+    rho0 = H.random_rho(N)
+    plan = engine.Plan(systems, grid, rho0, ops, tr, pt=pt)
+    plan.execute()
+    got = plan.download()
+    assert plan.info()[0] == MSPLIT and plan.info()[2] == 0
+    cmp_lists(got, oracle.propagate(systems, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
+
+
+def test_chi256_batch_beyond_one_launch_is_refused():
+    """chi = 256 has no batched fallback: a batch the groups cannot hold in one launch is refused at plan creation"""
+    N = 4
+    sysd, grid = H.random_system(N, n_steps=8, seed=3)
+    tr = Trajectories(np.zeros(300, dtype=int), np.full(300, 8))
+    pt = ptmod.random_pt(N, 256, D=9, n_slices=2, seed=1, eps=0.1)
+    with pytest.raises(Exception, match="chi 256"):
+        engine.Plan(sysd, grid, H.random_rho(N), [H.ketbra(N, 1, 1)], tr, pt=pt)

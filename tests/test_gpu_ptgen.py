@@ -491,3 +491,37 @@ def test_ptg_scratch_per_stream_and_convergence_on_last_sweep():
     assert ptgen_gpu.LAST_SWEEPS == need
     with pytest.raises(_lib.PQDError, match="no convergence"):
         ptgen_gpu.jacobi_cols(_dev(X.T), max_sweeps=need - 1)
+
+
+def test_tls_threshold_1e10_uncapped_bond_beats_the_cap_ibm(monkeypatch):
+    """at the tls phonon defaults (dt 0.1, a_e 5 nm, 4 K, K = 65 of the bath's own memory) a
+    threshold of 1e-10 asks for bonds up to ~160, past the batched kernel's cap of 128. Generated on the GPU with the
+    cap lifted to 256 (PQD_PT_MAX_BOND, the split groups' streamed-slice path), the cut is the threshold's (recorded:
+    no cap-bound cut) and the undriven dot's coherence is closer to the closed-form independent-boson solution over
+    40 ps than with the cap binding (host generator: 2.0e-5 against 3.0e-5 relative); at 1e-11 (bond ~200, still
+    the threshold's cut) it falls to 2.2e-6: the error falls with the threshold once the cap no longer decides."""
+    from pyaceqd_amd import ptgen_gpu
+    dt, n = 0.1, 400
+    J = lambda w: ptgen.qd_phonon_J(w, ae=5.0)  # noqa: E731
+    eta, delta = ptgen.eta_coefficients(J, 4.0, dt, 65)
+    t = dt * np.arange(n + 1)
+    ex = ptgen_oracle.ibm_coherence_exact(J, 4.0, t)
+
+    def run(thr, cap):
+        pt = ptgen_gpu.build_gaussian_pt_gpu(np.diag([0.0, 1.0]), dt, eta, delta, threshold=thr, max_bond=cap)
+        out = engine.propagate(System(dim=2, H0=np.zeros((2, 2))), Grid(0.0, dt, n), 0.5 * np.ones((2, 2), complex),
+                               [H.ketbra(2, 0, 1), np.eye(2)], Trajectories(np.array([0]), np.array([n])), pt=pt)[0]
+        assert np.max(np.abs(out[:, 1] - 1)) < 1e-9
+        return pt, float(np.max(np.abs(out[:, 0] - ex) / np.abs(ex)))
+
+    pt_free, e_free = run(1e-10, 256)
+    tr = pt_free.meta["truncation"]
+    assert pt_free.chi > 128 and not tr["cap_decided"] and tr["max_discarded_rel"] <= 1e-10
+    with pytest.warns(RuntimeWarning, match="bond cap 128"):
+        pt_cap, e_cap = run(1e-10, 128)
+    assert pt_cap.meta["truncation"]["cap_decided"]
+    pt_11, e_11 = run(1e-11, 256)
+    print(f"tls 1e-10: chi {pt_free.chi} err {e_free:.2e}; capped at 128 {e_cap:.2e}; 1e-11: chi {pt_11.chi} "
+          f"err {e_11:.2e}")
+    assert e_free < 2.6e-5 < e_cap < 3.2e-5 * 1.2
+    assert pt_11.chi > pt_free.chi and not pt_11.meta["truncation"]["cap_decided"] and e_11 < 5e-6
