@@ -49,6 +49,36 @@ __device__ __forceinline__ double2 c_group_sum(double2 v) {
     }
     return v;
 }
+// acc += pv(lane J of this lane's 16-lane row) * s, as c_fma (same order of the four products): v_fmac_f64 with its
+// first source taken by DPP row_newbcast, so a row value held once per row feeds the 16 lanes of the row. Every lane of
+// the wave must be active (the PT runs whole waves)
+template <int J>
+__device__ __forceinline__ void pq_cmac_bcast(double2& acc, const double2 pv, const double2 s) {
+    asm volatile(
+        "v_fmac_f64_dpp %0, %2, %4 row_newbcast:%c6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, -%3, %5 row_newbcast:%c6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %2, %5 row_newbcast:%c6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %3, %4 row_newbcast:%c6 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc.x), "+v"(acc.y)
+        : "v"(pv.x), "v"(pv.y), "v"(s.x), "v"(s.y), "i"(J));
+}
+// sum over j < KP of pv[j / 16](lane j % 16) * sreg[j]
+template <int J, int KP, int NPV, int NS>
+__device__ __forceinline__ void pq_row_bcast_mac(double2& acc, const double2 (&pv)[NPV], const double2 (&sreg)[NS]) {
+    if constexpr (J < KP) {
+        pq_cmac_bcast<J % 16>(acc, pv[J / 16], sreg[J]);
+        pq_row_bcast_mac<J + 1, KP>(acc, pv, sreg);
+    }
+}
+// a DPP source must not be written by a VALU instruction in the two cycles before it (the row values come from LDS
+// reads; this keeps two wait states after whatever the compiler puts between them and the products)
+template <int NPV>
+__device__ __forceinline__ void pq_dpp_src_ready(const double2 (&pv)[NPV]) {
+#pragma unroll
+    for (int c = 0; c < NPV; ++c) asm volatile("" ::"v"(pv[c].x), "v"(pv[c].y));
+    asm volatile("s_nop 1");
+}
+
 // x[l] + x[l ^ W] for W = 32 or 16 in every lane l, the same bits in both partners (each adds the same pair): gfx950's
 // v_permlane32_swap / v_permlane16_swap, one VALU move per 32-bit half instead of an LDS round trip. Whichever half
 // each swap moves, its two results hold x[l] and x[l ^ W] in some order, so their sum is the pair's.

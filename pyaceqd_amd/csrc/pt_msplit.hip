@@ -59,36 +59,6 @@ __device__ __forceinline__ void ms_st_sc1(double2* p, double2 v) {
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// acc += pv(lane J of this lane's 16-lane row) * s, as c_fma (same order of the four products): v_fmac_f64 with its
-// first source taken by DPP row_newbcast, so a row value held once per row feeds the 16 lanes of the row. Every lane of
-// the wave must be active (the PT runs whole waves)
-template <int J>
-__device__ __forceinline__ void ms_cmac_bcast(double2& acc, const double2 pv, const double2 s) {
-    asm volatile(
-        "v_fmac_f64_dpp %0, %2, %4 row_newbcast:%c6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, -%3, %5 row_newbcast:%c6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %2, %5 row_newbcast:%c6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %3, %4 row_newbcast:%c6 row_mask:0xf bank_mask:0xf"
-        : "+v"(acc.x), "+v"(acc.y)
-        : "v"(pv.x), "v"(pv.y), "v"(s.x), "v"(s.y), "i"(J));
-}
-// sum over j < KP of pv[j / 16](lane j % 16) * sreg[j]
-template <int J, int KP, int NPV, int NS>
-__device__ __forceinline__ void ms_pt_bcast(double2& acc, const double2 (&pv)[NPV], const double2 (&sreg)[NS]) {
-    if constexpr (J < KP) {
-        ms_cmac_bcast<J % 16>(acc, pv[J / 16], sreg[J]);
-        ms_pt_bcast<J + 1, KP>(acc, pv, sreg);
-    }
-}
-// a DPP source must not be written by a VALU instruction in the two cycles before it (the row values come from LDS
-// reads; this keeps two wait states after whatever the compiler puts between them and the products)
-template <int NPV>
-__device__ __forceinline__ void ms_nop_for(const double2 (&pv)[NPV]) {
-#pragma unroll
-    for (int c = 0; c < NPV; ++c) asm volatile("" ::"v"(pv[c].x), "v"(pv[c].y));
-    asm volatile("s_nop 1");
-}
-
 // sum over the 4 row groups of a gather column (lanes 8 / 16 apart at KPER = 8, 16 / 32 apart otherwise), left in all
 // four lanes with the same bits (each step adds the same pair: row_ror:8 inside a 16-lane row, then permlane swaps)
 template <int KP>
@@ -546,8 +516,8 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
                         const int b = b0 + u;
                         if (b >= TB || !((act >> b) & 1)) continue;
                         double2 acc = c_zero();
-                        ms_nop_for(pv[u]);
-                        ms_pt_bcast<0, KPER>(acc, pv[u], sreg);
+                        pq_dpp_src_ready(pv[u]);
+                        pq_row_bcast_mac<0, KPER>(acc, pv[u], sreg);
                         acc = make_double2(xor_add<16>(acc.x), xor_add<16>(acc.y));
                         acc = make_double2(xor_add<32>(acc.x), xor_add<32>(acc.y));
                         if (lane < 16) {

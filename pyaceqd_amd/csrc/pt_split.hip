@@ -359,8 +359,11 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
         if (!ow) {
             double2 acc = c_zero();
             if (rowg && fz && CHI == 64) {
-#pragma unroll
-                for (int j = 0; j < KPER; ++j) c_fma(acc, smem[PRT + kq * KPER + j], sreg[j]);
+                // the wave's 16 row values in lanes 0..15 of every 16-lane row, one ds_read_b128, taken by the products
+                // through DPP row_newbcast (16 broadcast reads before: one 4-cycle LDS instruction per complex MAC)
+                const double2 pv[1] = {smem[PRT + kq * KPER + (lane & 15)]};
+                pq_dpp_src_ready(pv);
+                pq_row_bcast_mac<0, KPER>(acc, pv, sreg);
             } else if (rowg && fz) {
 #pragma unroll
                 for (int j = 0; j < KPER; ++j) {
