@@ -258,9 +258,9 @@ def test_invalid_arguments_raise():
         engine.propagate(sysd, grid, H.ketbra(2, 0, 0), [np.eye(2)],
                          Trajectories(np.array([0]), np.array([5]), [MTO(0, 9, False, 1, np.eye(2))]))
     from pyaceqd_amd import _lib
-    with pytest.raises(_lib.PQDError, match="chi 129"):
+    with pytest.raises(_lib.PQDError, match="chi 257"):  # (129..256 run on split groups since round 6)
         engine.propagate(sysd, grid, H.ketbra(2, 0, 0), [np.eye(2)], Trajectories(np.array([0]), np.array([5])),
-                         pt=ptmod.random_pt(2, 129, n_slices=2))
+                         pt=ptmod.random_pt(2, 257, n_slices=2))
     s6, g6 = H.random_system(6, n_steps=3, seed=0)
     with pytest.raises(_lib.PQDError, match="CHI=128"):
         engine.propagate(s6, g6, H.ketbra(6, 0, 0), [np.eye(6)], Trajectories(np.array([0]), np.array([3])),
