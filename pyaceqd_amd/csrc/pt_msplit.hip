@@ -545,7 +545,7 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
         // (all of them unconditional but the slice rows: a path with fewer loads after the gather's would make the
         // waitcnt pass wait for the gather with a smaller count on every path)
         auto issue_ops = [&]() {
-            if constexpr (STAMP) {  // timing-only ablations (results not used): 128 no operand loads, 256 no closure
+            if constexpr (STAMP) {  // timing-only ablation (results not used): 128 no operand loads
                 if (!(p.ablate & 128)) load_ops(m + 1);
             } else {
                 load_ops(m + 1);  // entries past their window read rho0[0]

@@ -25,7 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n-t1", type=int, default=32)
     ap.add_argument("--n-tau", type=int, default=2000)
-    ap.add_argument("--ablate", type=int, default=0, help="extra PQD_ABLATE bits (timing only: 128 no operand loads, 1024 gather loads at element 0, 2048 per-workgroup rotation of the gather order)")
+    ap.add_argument("--ablate", type=int, default=0, help="extra PQD_ABLATE bits (timing only: 128 no operand loads, 1024 gather loads at element 0, 2048 per-workgroup rotation of the gather order, 8192 gather loads of hardware half 1 at element 0)")
     args = ap.parse_args()
     import bench
     from pyaceqd_amd import _lib, engine
