@@ -228,8 +228,9 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
     // [16 w + 4 blk + x]). The gather's roles are set in the step loop
     const int kq = (ht & 63) >> 4, j = 16 * (ht >> 6) + (ht & 15);
     const int grow = live ? p.gmap[alpha] : 0;
-    // chi = 128: the VALU path only (its slice row alone is 128 VGPRs); chi = 256 (STREAM): the slice row (1 MiB) is
-    // streamed from L2 through the matrix-core PT every step, 4 k-steps at a time, and sreg is unused
+    // chi = 128: the VALU path only (its slice row alone is 128 VGPRs; streaming it instead, as at chi = 256, removes
+    // the spills but measured slower: single run 51-53 ms against 42-45, profiles/r06/stream128/); chi = 256 (STREAM):
+    // the slice row (1 MiB) is streamed from L2 through the matrix-core PT every step, and sreg is unused
     constexpr bool STREAM = CHI > 128;
     const bool ptm = STREAM || (CHI <= 64 && q.ptm != 0);
     double2 sreg[STREAM ? 1 : KPER];
@@ -476,7 +477,7 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
                     // workgroup of the step reads the same slices)
                     const double2* __restrict__ Sg =
                         p.Q + ((size_t)cur_slice * p.D + grow) * CHI * CHI + (size_t)kq * CHI + j;
-                    constexpr int PFS = 4;
+                    constexpr int PFS = CHI > 128 ? 4 : 8;
                     for (int j0 = 0; j0 < KPER; j0 += PFS) {
                         double2 bq[PFS];
 #pragma unroll
