@@ -218,10 +218,11 @@ def test_msplit_spread_group_reruns_with_sc1_stores(monkeypatch):
 
 @pytest.mark.parametrize("N,chi", [(3, 32), (4, 64), (5, 32), (6, 64)])
 @pytest.mark.parametrize("ptm", ["0", "1"])
-@pytest.mark.parametrize("tb", ["1", "5", "8"])
+@pytest.mark.parametrize("tb", ["1", "5", "8", "12", "16"])
 def test_msplit_pt_on_valu_and_matrix_cores(monkeypatch, N, chi, ptm, tb):
     """the PT contraction on the FP64 VALU (DPP row broadcast) and on the matrix cores (3M 4x4x4_4b row blocks,
-    PQD_MS_PTM), with partial row blocks (TB = 1, 5) and inactive slots, vs the oracle"""
+    PQD_MS_PTM), with partial row blocks (TB = 1, 5) and inactive slots, up to the 16 trajectories per group auto mode
+    takes (two gather chunks per half, two row-block passes), vs the oracle"""
     monkeypatch.setenv("PQD_MSPLIT", "2")
     monkeypatch.setenv("PQD_MS_PTM", ptm)
     monkeypatch.setenv("PQD_MS_TB", tb)
