@@ -313,6 +313,35 @@ def run_c4_ntraj(steps, n_tau=2000, sizes=(16, 24, 32, 48, 64, 96, 128, 192, 256
     return {"config": "c4ntraj", "n_tau": n_tau, "rows": len(rows)}
 
 
+def run_msx(steps, n_tau=1000, sizes=(16, 32, 64, 128, 256)):
+    """the split-groups / batched crossover for the six-level model (N2 = 36, 18 workgroups of two rows per group):
+    `workload("sixls", ...)` with the t1 points of one scan point, chi = 64, on split groups forced (PQD_MSPLIT=2), in
+    auto mode and on the batched kernel (PQD_MSPLIT=0); us per grid step and the path taken"""
+    from pyaceqd_amd import engine
+    for n in sizes:
+        _, sysd, grid, pt, rho0, ops, tr = workload("sixls", 1, n, n_tau, 64)
+        row = {"model": "sixls", "n_traj": n, "grid_steps": grid.n_steps}
+        for label, env in (("msplit", {"PQD_MSPLIT": "2"}), ("auto", {}), ("batched", {"PQD_MSPLIT": "0"})):
+            for k, v in env.items():
+                os.environ[k] = v
+            try:
+                plan = engine.Plan(sysd, grid, rho0, ops, tr, pt=pt)
+            finally:
+                for k in env:
+                    os.environ.pop(k)
+            plan.execute()
+            plan.synchronize()
+            plan.timing(reset=True)
+            for _ in range(steps):
+                plan.execute()
+            plan.synchronize()
+            _, ms, _ = plan.timing(reset=True)
+            path, bt, _ = plan.info()
+            row[label] = {"path": path, "bt": bt, "us_per_step": ms * 1e3 / (grid.n_steps + 1)}
+        print(json.dumps(row), flush=True)
+    return {"config": "msx", "n_tau": n_tau}
+
+
 def run_c5dm(steps, n_e0=2, bxs=(0.0, 1.0, 2.0, 4.0), tend=400.0):
     import tempfile
     from pyaceqd_amd import opgrammar, pt as ptmod
@@ -356,7 +385,7 @@ def main():
     for name in args.configs.split(","):
         # c5dm32: one rank's share of SURVEY §8d C5 (256 points = 64 e0 x 4 bx over 8 GPUs): 8 e0 x 4 bx
         special = {"c5dm": run_c5dm, "c4reuse": run_c4reuse, "c5dm32": lambda st: run_c5dm(st, n_e0=8),
-                   "c4full": run_c4_literal, "c4ntraj": run_c4_ntraj,
+                   "c4full": run_c4_literal, "c4ntraj": run_c4_ntraj, "msx": run_msx,
                    "c4shard": lambda st: run_c4_literal(st, n_t1=32, t1_offset=96, name="c4shard")}
         print(json.dumps(special[name](args.steps) if name in special else run(name, args.steps)), flush=True)
 
