@@ -900,7 +900,17 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
             const int G = msplit_group_size(N2, P->CHI);
             const int resident = n_cu * bpc / G;          // groups the device holds at once
             const int gps = 32 / G;                        // groups per XCD slot (32 CUs per XCD on MI355X)
-            const int max_groups = std::min(resident, gps >= 1 ? 8 * gps : resident);
+            // PQD_SPLIT_XCD=0: the plain grid (groups may span XCDs, sc1 exchange), as many groups as are resident
+            bool xgrid = [] { const char* x = getenv("PQD_SPLIT_XCD"); return !(x && atoi(x) == 0); }();
+            // where the XCD slots hold fewer groups than the device (G > 16: one group of 18 per 32 CUs at N2 = 36)
+            // and that leaves more than 8 trajectories per group, the plain grid's extra groups pay for its cross-XCD
+            // exchange (six-level, 128 trajectories: 11.6 against 14.6 us per grid step; equal at 64, slower below,
+            // profiles/r06/msx2/)
+            if (xgrid && gps >= 1 && 8 * gps < resident) {
+                const int tbx = (tr->n_traj + 8 * gps - 1) / (8 * gps), tbp = (tr->n_traj + resident - 1) / resident;
+                if (tbx > 8 && tbp < tbx) xgrid = false;
+            }
+            const int max_groups = std::min(resident, (xgrid && gps >= 1) ? 8 * gps : resident);
             int TB = (tr->n_traj + max_groups - 1) / std::max(1, max_groups);
             if (const char* f = getenv("PQD_MS_TB")) TB = std::max(TB, atoi(f));
             const int n_groups = (tr->n_traj + TB - 1) / TB;
@@ -936,7 +946,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
                 P->msplit = true;
                 ms_TB = TB;
                 ms_groups = n_groups;
-                ms_xcd = (gps >= 1 && n_groups <= 8 * gps) ? (n_groups + 7) / 8 : 0;
+                ms_xcd = (xgrid && gps >= 1 && n_groups <= 8 * gps) ? (n_groups + 7) / 8 : 0;
                 if (const char* x = getenv("PQD_SPLIT_XCD"); x && atoi(x) == 0) ms_xcd = 0;
             }
         }
