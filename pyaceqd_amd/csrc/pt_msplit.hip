@@ -535,7 +535,13 @@ __global__ __launch_bounds__(4 * CHI * R) void pt_msplit_kernel(SweepParams p, M
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) __hip_atomic_store((mu32*)(ct + g), ((unsigned)n + 1u) | xtag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) {
+            // with the group's placement on one XCD verified (first poll, l2keep) the arrival word is a plain store
+            // too: its line stays in the group's L2, where the peers' sc1 polls find it without a fabric round trip
+            const unsigned av = ((unsigned)n + 1u) | xtag;
+            if (q.l2keep && n >= 1) *(__attribute__((address_space(1))) unsigned*)(ct + g) = av;
+            else __hip_atomic_store((mu32*)(ct + g), av, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         stamp(n, 2);
         // ---- operands of step n + 1 (loaded during step n - 1's gather) to LDS
         stage_ops();
