@@ -179,6 +179,8 @@ struct SweepParams {
     int traj_base;           // split groups: trajectory of group 0 (a batch run as several co-resident launches)
     int split_xcd;           // split groups, set per launch: > 0 = trajectories in this launch, each group's workgroups
                              //   dealt onto one XCD (blocks b with equal b % 8; speed only, PQD_SPLIT_XCD=0 off)
+    int split_l2;            // split groups on the XCD-grouped grid: exchange lines kept in the group's L2 (placement
+                             //   checked at the first poll; PQD_SPLIT_L2=0: sc1 stores)
     int n_steps;             // grid steps (operand prefetch bound)
     int n_blk;               // blocks of the launch (quad kernel: quads; tail workgroups check it)
     int qprio;               // quad kernel wave priorities (PQD_QPRIO, A/B): bit 0 first half of the grid above the

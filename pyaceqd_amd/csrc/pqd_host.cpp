@@ -1125,6 +1125,7 @@ int pqd_plan_create_multi(pqd_ctx* ctx, int32_t n_sys, const pqd_system* systems
     { const char* b1 = getenv("PQD_SPLIT_GRAN"); sp.split_gran = (b1 && atoi(b1) == 1) ? 1 : 0; }
     sp.split_ow = split_ow_env() ? 1 : 0;  // the output workgroup (pt_split.hip OWG); split_group_size agrees
     { const char* b2 = getenv("PQD_SPLIT_XCD"); sp.split_xcd = (b2 && atoi(b2) == 0) ? 0 : 1; }
+    { const char* b3 = getenv("PQD_SPLIT_L2"); sp.split_l2 = (b3 && atoi(b3) == 0) ? 0 : 1; }
     // polls of a split group's counter before the wait counts as a timeout (~0.1 s); PQD_SPLIT_SPIN overrides
     // it (tests provoke the batched fallback with 0)
     { const char* sl = getenv("PQD_SPLIT_SPIN"); sp.spin_limit = sl ? (unsigned)strtoul(sl, nullptr, 10) : (1u << 22); }

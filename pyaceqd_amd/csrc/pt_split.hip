@@ -136,12 +136,28 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
     // add per arrival, G per step) measured faster (C5 single run 43.1 -> 38.6-40.5 ms, profiles/r05/hyb/)
     constexpr bool FLAGS = G <= 32;
     unsigned* ct = cnt + (size_t)t * 64;
+    // l2k (counter form with flags, XCD-grouped grid): the payload and, from the second step on, the arrival words are
+    // plain stores that keep their lines in the group's L2, where the peers' sc1 loads find them. That is coherent only
+    // if the whole group runs on one XCD: every flag carries its writer's XCD id (bits 28..30, HW_REG_XCC_ID) and the
+    // first poll checks them; a group spread over XCDs ends the launch before its first gather (error word), and the
+    // host re-runs it on the batched kernel. PQD_ABLATE bit 512 fakes a spread group (workgroup 0 reports the next XCD)
+    const bool l2k = FLAGS && !GRAN && p.split_xcd > 0 && p.split_l2 != 0;
+    unsigned xtag = 0;
+    if (l2k) {
+        unsigned xid = (unsigned)__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;  // hwreg(HW_REG_XCC_ID, 0, 4)
+        if ((p.ablate & 512) && g == 0) xid = (xid + 1u) & 7u;
+        xtag = xid << 28;
+    }
     auto arrive = [&](int n) {
-        if constexpr (FLAGS)
-            __hip_atomic_store((gu32*)(ct + g), (unsigned)n + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
+        if constexpr (FLAGS) {
+            const unsigned av = ((unsigned)n + 1u) | xtag;
+            if (l2k && n >= 1) *(__attribute__((address_space(1))) unsigned*)(ct + g) = av;
+            else __hip_atomic_store((gu32*)(ct + g), av, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
             __hip_atomic_fetch_add((gu32*)ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     };
+    bool placed_checked = false;
     const int n_end = we;
     constexpr int m2 = N2 * N2;
     const int ev_lim = p.ev_start[t + 1];
@@ -398,7 +414,12 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
                     double2 y = smem[REDO + tid];
 #pragma unroll
                     for (int q = 1; q < KG; ++q) y = c_add(y, smem[REDO + q * CHI + tid]);
-                    st_sc1(Xn + (size_t)g * CHI + tid, y);
+                    if (l2k) {
+                        typedef double v2f64 __attribute__((ext_vector_type(2)));
+                        *(__attribute__((address_space(1))) v2f64*)(Xn + (size_t)g * CHI + tid) = v2f64{y.x, y.y};
+                    } else {
+                        st_sc1(Xn + (size_t)g * CHI + tid, y);
+                    }
                 }
                 // ---- arrive (every storing wave drained, then one lane); the wait for the group is below
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -492,7 +513,13 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
                         const unsigned v =
                             lane < G ? __hip_atomic_load((gu32*)(ct + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                      : want;
-                        if (__all(v >= want)) break;
+                        if (__all((v & 0x0FFFFFFFu) >= want)) {
+                            if (l2k && !placed_checked) {  // the same words reach every workgroup: one decision
+                                const unsigned x0 = __builtin_amdgcn_readfirstlane(v) >> 28;
+                                if (!__all(lane >= G || (v >> 28) == x0)) { ok = false; break; }
+                            }
+                            break;
+                        }
                     } else {
                         if (__hip_atomic_load((gu32*)ct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)G * want)
                             break;
@@ -505,6 +532,7 @@ __global__ __launch_bounds__(SP_NT) void pt_split_kernel(SweepParams p, double2*
                     if (!ok) __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
+            placed_checked = true;
             __syncthreads();
             if (s_abort) return;
             stamp(n, 5);

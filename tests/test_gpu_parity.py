@@ -109,6 +109,35 @@ def test_sweep_pt_split_groups(monkeypatch, N, chi, split):
 
 
 @pytest.mark.parametrize("N", [3, 4, 6])
+@pytest.mark.parametrize("mode", ["l2sc1", "spread"])
+def test_sweep_pt_split_groups_exchange_flavours(monkeypatch, N, mode):
+    """the counter exchange on the XCD-grouped grid with sc1 stores (PQD_SPLIT_L2=0) instead of the L2-kept lines,
+    and a group that reports a spread placement (PQD_ABLATE=512: workgroup 0 claims the next XCD; the first poll sees
+    it, the launch ends before its first gather and the plan re-runs the batch on the batched kernel), vs the oracle"""
+    monkeypatch.setenv("PQD_SPLIT", "2")
+    if mode == "l2sc1":
+        monkeypatch.setenv("PQD_SPLIT_L2", "0")
+    else:
+        monkeypatch.setenv("PQD_ABLATE", "512")
+    systems = [H.random_system(N, n_steps=30, seed=50 + k)[0] for k in range(2)]
+    grid = Grid(0.0, 0.1, 30)
+    n_traj = max(1, min(5, 256 // (N * N + 1)))
+    tr = _traj(grid.n_steps, N, n_traj, seed=2 * N + 1)
+    tr.system = np.array([k % 2 for k in range(n_traj)])
+    pt = ptmod.random_pt(N, 64, D=min(N * N, 9), n_slices=6, seed=N, eps=0.15)
+    ops = [H.ketbra(N, 0, 0), H.ketbra(N, 1, 0), np.eye(N)]
+    rho0 = H.random_rho(N)
+    plan = engine.Plan(systems, grid, rho0, ops, tr, pt=pt)
+    plan.execute()
+    got = plan.download()
+    if mode == "l2sc1" or N * N + 1 > 32:  # (groups of more than 32 workgroups keep one counter and sc1 stores)
+        assert plan.info()[0] == "split groups" and plan.info()[2] == 0
+    else:
+        assert plan.info()[2] == 1 and plan.info()[0] == "batched lock-step sweep"
+    cmp_lists(got, oracle.propagate(systems, grid, rho0, ops, tr, pt=pt, nthreads=8), 1e-11)
+
+
+@pytest.mark.parametrize("N", [3, 4, 6])
 def test_sweep_pt_split_groups_in_consecutive_launches(N):
     """a small batch just above the co-resident capacity (n_traj * N^2 > CUs) runs its split groups as consecutive
     launches (auto mode): same outputs as the oracle and the batched kernel, and the plan reports split groups"""
